@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""Benchmark of the device-resident packet-record path (BASELINE.json metric).
+
+Workload (config 3 of BASELINE.json, the largest single-GPU config): per GPU,
+100M synthetic IPv4/TCP frames, IMIX 64/576/1500 B at 7:4:1 (35.4 GB arena),
+10k flows, all resident in HBM before the timed region. A step = one
+``tcbee_parse_batch_device`` over the whole batch: parse + 74-B records +
+flow hash + flow classification (table upsert, dense first-seen ids) +
+counters. With --gpus N each rank parses its own contiguous shard of one global
+trace (weak scaling, no data-path collective); the per-rank counters are summed
+over RCCL once per step.
+
+Prints ONE JSON line (rank 0). See DESIGN.md "Measurement".
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mpkt/s device-resident TCP header parse+flow-classify, 64–1500B frames"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+IDX_BYTES = 8 + 4 + 8          # offset u64 + caplen u32 + ts_ns u64 read per frame
+V4_HDR_BYTES = 54              # eth + ipv4 + tcp header bytes the hook reads
+OUT_BYTES = 74 + 4 + 4         # record + flow hash + flow id (slot) written per record
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_device_trace(torch, n, sizes, kind, n_flows, seed, first_index, stream):
+    """Synthetic trace straight into HBM: index on the host (numpy), headers by the
+    device generator (bit-identical to the host generator)."""
+    import tcbee_amd
+    off, ln, ts, alen = tcbee_amd.synth_index(n, sizes=sizes, seed=seed, first_index=first_index)
+    d_arena = torch.zeros(alen + 64, dtype=torch.uint8, device="cuda")
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    d_len = torch.from_numpy(ln.view(np.int32)).cuda()
+    d_ts = torch.from_numpy(ts.view(np.int64)).cuda()
+    tcbee_amd.gen_frames_device(d_arena, d_off, d_len, n, kind, n_flows, seed, stream=stream,
+                                first_index=first_index)
+    torch.cuda.synchronize()
+    return d_arena, alen, d_off, d_len, d_ts
+
+
+def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup, seed):
+    import tcbee_amd
+    stream = torch.cuda.current_stream().cuda_stream
+    first = rank * n
+    d_arena, alen, d_off, d_len, d_ts = build_device_trace(torch, n, sizes, kind, n_flows,
+                                                           seed, first, stream)
+    d_rec = torch.empty(n * 74 + 64, dtype=torch.uint8, device="cuda")
+    d_hash = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_id = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_n = torch.zeros(1, dtype=torch.int64, device="cuda")
+    d_ctr = torch.zeros(4, dtype=torch.int64, device="cuda")
+    p = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=n, max_arena=0,
+                               max_flows=max(4 * n_flows, 1 << 12))
+
+    def step():
+        p.parse_device(d_arena, alen, d_off, d_len, d_ts, n, d_rec, n, d_hash, d_id, d_n,
+                       d_ctr, stream=stream)
+        if world > 1:
+            dist.all_reduce(d_ctr)  # RCCL: global INGRESS/HANDLED/DROPPED
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    p.profile(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    k1_ms, k1_launches = p.profile_read()
+    elapsed = t1 - t0
+    status = p.status()
+
+    # validation (untimed): counts, flow table, and a bit-exact sample vs the oracle
+    nrec = int(d_n.item())
+    flows = p.flows()
+    check = {"records": nrec, "flows": int(len(flows)), "status": status}
+    if rank == 0:
+        check.update(validate_sample(torch, d_rec, d_hash, n, sizes, kind, n_flows, seed,
+                                     first, nrec))
+    p.close()
+    del d_arena, d_rec
+    torch.cuda.empty_cache()
+    return elapsed, k1_ms / max(k1_launches, 1), nrec, check
+
+
+def validate_sample(torch, d_rec, d_hash, n, sizes, kind, n_flows, seed, first, nrec,
+                    sample=200_000):
+    """Records [0, sample) and the last `sample` records vs the oracle on the same frames."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import tcbee_amd
+    from oracle_py import Oracle
+    orc = Oracle()
+    ok = True
+    for lo in (0, max(0, n - sample)):
+        hi = min(n, lo + sample)
+        tr = tcbee_amd.synth_trace(hi - lo, sizes=sizes, kind=kind, n_flows=n_flows, seed=seed,
+                                   first_index=first + lo)
+        rec, fh, _, _, _ = orc.parse(tr)
+        # synthetic frames are all accepted, so record index == frame index
+        g = d_rec[lo * 74: hi * 74].cpu().numpy().reshape(-1, 74)
+        gh = d_hash[lo:hi].cpu().numpy().view(np.uint32)
+        ok = ok and len(rec) == hi - lo and np.array_equal(g, rec) and np.array_equal(gh, fh)
+    return {"sample_bit_exact": bool(ok and nrec == n), "sample_frames": 2 * sample}
+
+
+def cpu_baseline(sizes, kind, n_flows, seed, seconds, threads, sample_n=2_000_000):
+    """The reference record path restated in C (oracle), timed on host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import tcbee_amd
+    from oracle_py import Oracle
+    orc = Oracle()
+    tr = tcbee_amd.synth_trace(sample_n, sizes=sizes, kind=kind, n_flows=n_flows, seed=seed)
+    out = {}
+    for t in sorted({1, threads}):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            orc.baseline(tr, threads=t)
+            done += tr.n
+            el = time.perf_counter() - t0
+            if el >= seconds / (2 if t == 1 and threads > 1 else 1):
+                break
+        out[t] = (done / el / 1e6, done, el)
+    return out, tr.n
+
+
+def host_path_e2e(sizes, kind, n_flows, seed, n=4_000_000, reps=3):
+    """End-to-end rate through the host-pointer entry point: pageable H2D of the frames,
+    parse, D2H of records + flow hash/id (tcbee_parse_batch)."""
+    import tcbee_amd
+    tr = tcbee_amd.synth_trace(n, sizes=sizes, kind=kind, n_flows=n_flows, seed=seed)
+    with tcbee_amd.PacketParser(max_frames=n, max_arena=len(tr.arena),
+                                max_flows=max(4 * n_flows, 1 << 12)) as p:
+        p.parse(tr)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = p.parse(tr)
+        el = (time.perf_counter() - t0) / reps
+    return {"mpkts": n / el / 1e6, "frames": n, "bytes_h2d": int(len(tr.arena)) + 20 * n,
+            "records": r.n}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=100_000_000, help="frames per GPU")
+    ap.add_argument("--sizes", default="imix", choices=["imix", "64"])
+    ap.add_argument("--flows", type=int, default=10_000)
+    ap.add_argument("--seed", type=int, default=0x7CBEE)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip config-2 and e2e legs")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    kind = 1 if args.flows > 1 else 0
+
+    elapsed, k1_ms, nrec, check = run_device(torch, dist, rank, world, args.frames, args.sizes,
+                                             kind, args.flows, args.steps, args.warmup,
+                                             args.seed)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    total_frames = args.frames * world * args.steps
+    value = total_frames / elapsed / 1e6
+
+    out = None
+    if rank == 0:
+        # roofline of the dominant kernel (K1 k_parse), algorithmic bytes per launch
+        hdr = V4_HDR_BYTES  # synthetic frames are IPv4/TCP
+        alg_bytes = args.frames * (IDX_BYTES + hdr) + nrec * OUT_BYTES
+        achieved = alg_bytes / (k1_ms * 1e-3) / 1e9
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "Mpkt/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": ("config3: IMIX 64/576/1500 7:4:1 IPv4/TCP, "
+                                    f"{args.flows} flows" if args.sizes == "imix"
+                                    else f"64B IPv4/TCP, {args.flows} flow(s)"),
+                       "frames_per_gpu": args.frames, "flows": args.flows,
+                       "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "kernel": "k_parse",
+                         "k1_ms": round(k1_ms, 4),
+                         "alg_bytes_per_frame": IDX_BYTES + hdr + OUT_BYTES},
+            "check": check,
+        }
+        if not args.no_extra and world == 1:
+            e_el, e_k1, e_n, e_chk = run_device(torch, None, 0, 1, 1_000_000, "64", 0, 1,
+                                                max(args.steps, 20), args.warmup, args.seed)
+            out["config2_1M_64B"] = {"mpkts": round(1_000_000 * max(args.steps, 20) / e_el / 1e6, 1),
+                                     "ms_per_step": round(e_el / max(args.steps, 20) * 1e3, 4),
+                                     "k1_ms": round(e_k1, 4), "check": e_chk}
+            out["e2e_host_path"] = host_path_e2e(args.sizes, kind, args.flows, args.seed)
+        if not args.no_cpu and world == 1:
+            threads = min(16, os.cpu_count() or 1)
+            res, sample_n = cpu_baseline(args.sizes, kind, args.flows, args.seed,
+                                         args.cpu_seconds, threads)
+            v, done, el = res[threads]
+            out["cpu_baseline"] = {
+                "value": round(v, 2), "unit": "Mpkt/s", "cores": threads, "kind": "port",
+                "sample": (f"{sample_n} frames of the same workload, repeated {done // sample_n}x "
+                           f"({el:.1f}s); oracle/tcbee_oracle.c orc_baseline_run = xdp_hook + "
+                           "per-thread FLOWS(100) + bincode serialize"),
+                "single_thread": round(res[1][0], 2)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,205 @@
+/*
+ * tcbee_amd.h — C ABI of the MI355X-native TCBee packet-record path.
+ *
+ * What this replaces (all paths relative to the TCBee reference tree):
+ *   - the per-packet kernel hooks  xdp_packet_tracer / tc_packet_tracer
+ *       tcbee-record/tcbee-ebpf/src/main.rs:69-83
+ *     which call xdp_hook / tc_hook
+ *       tcbee-record/tcbee-ebpf/src/probes/xdp.rs:27-223
+ *       tcbee-record/tcbee-ebpf/src/probes/tc.rs:28-183
+ *   - the FLOWS flow set they insert into
+ *       tcbee-record/tcbee-ebpf/src/flow_tracker.rs:12-23
+ *   - the counters they bump (INGRESS/EGRESS_EVENTS, EVENTS_HANDLED/DROPPED)
+ *       tcbee-record/tcbee-ebpf/src/counters.rs:5-83
+ *   - the user-space serializer that turns each ring entry into the on-disk
+ *     74-byte record (bincode fixint-LE 70 B + FF FF FF FF)
+ *       tcbee-record/tcbee/src/handlers/mod.rs:94-146
+ *
+ * The kernel hook ABI is one call per packet; this ABI is one call per BATCH of
+ * frames. Output is the 74-byte *file* layout (what tcbee-process reads,
+ * tcbee-process/src/bindings/tcp_packet.rs:8-43), compacted, in input order.
+ *
+ * Conventions
+ *   - Every function returns 0 (TCBEE_OK) or a negative TCBEE_E* code; nothing
+ *     throws across the ABI.
+ *   - All buffers are caller-owned; nothing is allocated inside a parse call.
+ *   - One tcbee_ctx per host thread / HIP stream. Calls on different contexts
+ *     are independent.
+ *   - "_device" entry points take DEVICE pointers and a hipStream_t (as void*,
+ *     NULL = the context's own stream) and are asynchronous unless stated.
+ *     Host-pointer entry points copy H2D / D2H through the context's buffers.
+ */
+#ifndef TCBEE_AMD_H
+#define TCBEE_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TCBEE_ABI_VERSION 1
+
+/* ---- record / key layout constants (DESIGN.md "Data layout") ------------ */
+#define TCBEE_RECORD_BYTES   74  /* tcp_packet.rs:42 ENTRY_SIZE            */
+#define TCBEE_TRACE_BYTES    72  /* repr(C) tcp_packet_trace, tcp_header.rs:554-572 */
+#define TCBEE_IPTUPLE_BYTES  38  /* repr(C) IpTuple, flow.rs:4-12          */
+#define TCBEE_KEY_BYTES      40  /* IpTuple + 2 zero bytes (hash/table key) */
+#define TCBEE_MAX_HDR_BYTES  74  /* eth 14 + ipv6 40 + tcp 20              */
+#define TCBEE_REF_MAX_FLOWS 100  /* config.rs:19 MAX_FLOWS                  */
+
+/* ---- error codes --------------------------------------------------------- */
+#define TCBEE_OK                  0
+#define TCBEE_EINVAL             -1  /* bad argument                          */
+#define TCBEE_ENOMEM             -2  /* device / host allocation failed        */
+#define TCBEE_EDEVICE            -3  /* HIP runtime error                      */
+#define TCBEE_ECAPACITY          -4  /* batch larger than the context was made for */
+#define TCBEE_EFLOWFULL          -5  /* flow table full (records still written) */
+#define TCBEE_ENODEV             -6  /* no HIP device                           */
+#define TCBEE_EIO                -7  /* file I/O error                          */
+#define TCBEE_EFORMAT            -8  /* malformed input file                    */
+#define TCBEE_ESPIN              -9  /* a bounded in-kernel wait timed out      */
+
+/* ---- directions (which hook / which output file) ------------------------- */
+#define TCBEE_DIR_INGRESS 0  /* xdp_hook  -> xdp.tcp, counts INGRESS_EVENTS */
+#define TCBEE_DIR_EGRESS  1  /* tc_hook   -> tc.tcp,  counts EGRESS_EVENTS  */
+
+/* ---- cfg flags ------------------------------------------------------------ */
+#define TCBEE_F_NO_FLOWS     0x1u /* skip flow classification (hash/id/table) */
+
+typedef struct tcbee_ctx tcbee_ctx;
+
+/* Load-time configuration of the hook.
+ * filter_port: the FILTER_PORT global (tcbee-ebpf/src/main.rs:30-31), set by
+ *   EbpfLoader::set_global (tcbee/src/eBPF/ebpf_runner.rs:79-84). Host order;
+ *   0 = no filter; otherwise a frame is kept only if sport or dport equals it
+ *   (xdp.rs:89-92, tc.rs:72-77). */
+typedef struct tcbee_cfg {
+    uint16_t filter_port;
+    uint8_t  direction;      /* TCBEE_DIR_*                               */
+    uint8_t  reserved0;
+    uint32_t flags;          /* TCBEE_F_*                                 */
+} tcbee_cfg;
+
+/* A batch of raw Ethernet frames ("the packet as XDP/TC sees it").
+ * Frame i occupies arena[offset[i] .. offset[i] + caplen[i]).
+ * ts_ns[i] replaces bpf_ktime_get_ns() (xdp.rs:95, tc.rs:80): a replay cannot
+ * reproduce the hook-time clock, so the record carries the trace timestamp.
+ * The arena may be followed by anything; the kernel never reads past
+ * arena_len. */
+typedef struct tcbee_frames {
+    const uint8_t*  arena;
+    uint64_t        arena_len;
+    const uint64_t* offset;
+    const uint32_t* caplen;
+    const uint64_t* ts_ns;
+    uint64_t        n;
+} tcbee_frames;
+
+/* Counters of counters.rs, summed over CPUs the way the TUI does
+ * (tcbee/src/viz/rate_watcher.rs:52-76), widened to u64 (no wrap). */
+typedef struct tcbee_counters {
+    uint64_t ingress;   /* INGRESS_EVENTS: accepted TCP frames, direction 0 */
+    uint64_t egress;    /* EGRESS_EVENTS:  accepted TCP frames, direction 1 */
+    uint64_t handled;   /* EVENTS_HANDLED: records written                  */
+    uint64_t dropped;   /* EVENTS_DROPPED: accepted but no output room      */
+} tcbee_counters;
+
+/* One flow of the context's flow table (64 B).
+ * tuple = IpTuple repr(C) bytes (flow.rs:4-12; v4 address = 12 zero bytes +
+ * 4 wire bytes, xdp.rs:116-119) followed by 2 zero bytes. Flow ids are dense,
+ * assigned in first-seen order over the whole record stream of the context
+ * (the order in which tcbee-process creates flows, db_writer.rs:51-65). */
+typedef struct tcbee_flow_entry {
+    uint8_t  tuple[TCBEE_KEY_BYTES];
+    uint64_t pkts;        /* records of this flow                         */
+    uint64_t bytes;       /* sum of caplen of those frames                */
+    uint64_t first_seen;  /* global record index of its first record      */
+} tcbee_flow_entry;
+
+/* ---- library ------------------------------------------------------------- */
+int         tcbee_abi_version(void);
+const char* tcbee_strerror(int code);
+/* Number of HIP devices visible (0 if none). Safe to call without a GPU. */
+int         tcbee_device_count(int* n);
+
+/* ---- context --------------------------------------------------------------
+ * max_frames: largest batch (frames) any parse call on this ctx will pass.
+ * max_arena : largest arena (bytes) the HOST entry point will copy.
+ * max_flows : flow-table capacity in distinct flows (table has >= 2x slots).
+ * device    : HIP device ordinal. */
+int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames,
+                     uint64_t max_arena, uint64_t max_flows);
+int tcbee_ctx_destroy(tcbee_ctx* ctx);
+/* The context's own HIP stream (hipStream_t as void*). */
+int tcbee_ctx_stream(tcbee_ctx* ctx, void** stream);
+int tcbee_ctx_sync(tcbee_ctx* ctx);
+
+/* ---- the hot path (device-resident) ---------------------------------------
+ * Parses in_dev->n frames that already live in HBM. Writes, in input order and
+ * compacted to accepted frames only:
+ *   out_rec74     [out_cap * 74] bytes  — tcbee-process record layout
+ *   out_flow_hash [out_cap] u32          — tcbee flow hash v1 of the IpTuple
+ *   out_flow_id   [out_cap] u32          — dense first-seen flow id
+ * (flow outputs may be NULL, and are skipped entirely with TCBEE_F_NO_FLOWS).
+ * out_n_dev (device u64) receives the number of records written;
+ * ctr_dev (device tcbee_counters) is ACCUMULATED into (zero it once).
+ * Asynchronous on `stream`; the flow table of ctx is updated in place.
+ * in_dev is a host struct whose pointers are device pointers. */
+int tcbee_parse_batch_device(tcbee_ctx* ctx, const tcbee_frames* in_dev,
+                             const tcbee_cfg* cfg,
+                             uint8_t* out_rec74, uint64_t out_cap,
+                             uint32_t* out_flow_hash, uint32_t* out_flow_id,
+                             uint64_t* out_n_dev, tcbee_counters* ctr_dev,
+                             void* stream);
+
+/* Same, host buffers in and out (H2D of frames, D2H of records), synchronous.
+ * out_n / ctr are host pointers; ctr is accumulated into. */
+int tcbee_parse_batch(tcbee_ctx* ctx, const tcbee_frames* in_host,
+                      const tcbee_cfg* cfg,
+                      uint8_t* out_rec74, uint64_t out_cap,
+                      uint32_t* out_flow_hash, uint32_t* out_flow_id,
+                      uint64_t* out_n, tcbee_counters* ctr);
+
+/* ---- flow table ------------------------------------------------------------ */
+/* Synchronous. Number of distinct flows seen so far / export in id order. */
+int tcbee_flow_count(tcbee_ctx* ctx, uint64_t* n);
+int tcbee_flow_export(tcbee_ctx* ctx, tcbee_flow_entry* out_host, uint64_t cap,
+                      uint64_t* n);
+/* Forget every flow (ids restart at 0, record index restarts at 0). */
+int tcbee_flow_reset(tcbee_ctx* ctx);
+/* Sticky status of the last batches: TCBEE_OK, TCBEE_EFLOWFULL or TCBEE_ESPIN.
+ * Synchronous; clears the status. */
+int tcbee_ctx_status(tcbee_ctx* ctx);
+
+/* ---- measurement ------------------------------------------------------------
+ * When enabled, every parse call records a HIP event pair around K1 (the parse
+ * kernel) on the stream it is launched on. profile_read synchronizes those
+ * events and returns the summed K1 time and the number of K1 launches since the
+ * last enable (up to 4096 launches are kept). */
+int tcbee_ctx_profile(tcbee_ctx* ctx, int enable);
+int tcbee_ctx_profile_read(tcbee_ctx* ctx, double* k1_ms_total, uint64_t* k1_launches);
+
+/* ---- synthetic trace generator (device) -----------------------------------
+ * Fills the header bytes of frames whose offset/caplen are already on the
+ * device (see DESIGN.md "Synthetic traces"); local frame j is global frame
+ * first_index + j. kind 0 = config-2 single flow, kind 1 = multi-flow IPv4
+ * (flow of frame i = splitmix64(seed + 0x1000 + i) % n_flows). Payload bytes are
+ * left as they are (callers zero the arena). Asynchronous on stream. */
+int tcbee_gen_frames_device(uint8_t* arena_dev, const uint64_t* offset_dev,
+                            const uint32_t* caplen_dev, uint64_t n,
+                            uint64_t first_index, int kind, uint64_t n_flows,
+                            uint64_t seed, void* stream);
+/* The same frames on the host (bit-identical to the device generator). */
+int tcbee_gen_frames_host(uint8_t* arena, const uint64_t* offset,
+                          const uint32_t* caplen, uint64_t n, uint64_t first_index,
+                          int kind, uint64_t n_flows, uint64_t seed);
+
+/* ---- host utilities (no GPU needed) ------------------------------------- */
+/* tcbee flow hash v1 of a 40-byte key (DESIGN.md "Flow hash"). */
+uint64_t tcbee_flow_hash64(const uint8_t key40[TCBEE_KEY_BYTES]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TCBEE_AMD_H */

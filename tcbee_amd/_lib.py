@@ -1,0 +1,136 @@
+"""ctypes binding of libtcbee_amd.so (the C ABI in include/tcbee_amd.h).
+
+The shared library is built in-tree (tcbee_amd/lib/libtcbee_amd.so) by
+``__graft_entry__.build()`` / ``make -C tcbee_amd/csrc``. There is no fallback:
+if the library is missing, importing the product path raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libtcbee_amd.so")
+
+RECORD_BYTES = 74
+TRACE_BYTES = 72
+KEY_BYTES = 40
+DIR_INGRESS = 0
+DIR_EGRESS = 1
+F_NO_FLOWS = 0x1
+
+OK = 0
+EINVAL = -1
+ENOMEM = -2
+EDEVICE = -3
+ECAPACITY = -4
+EFLOWFULL = -5
+ENODEV = -6
+EIO = -7
+EFORMAT = -8
+ESPIN = -9
+
+
+class TcbeeError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = _strerror(code)
+        super().__init__(f"{what}: {msg} ({code})" if what else f"{msg} ({code})")
+
+
+class Cfg(C.Structure):
+    _fields_ = [("filter_port", C.c_uint16), ("direction", C.c_uint8),
+                ("reserved0", C.c_uint8), ("flags", C.c_uint32)]
+
+
+class Frames(C.Structure):
+    _fields_ = [("arena", C.c_void_p), ("arena_len", C.c_uint64),
+                ("offset", C.c_void_p), ("caplen", C.c_void_p),
+                ("ts_ns", C.c_void_p), ("n", C.c_uint64)]
+
+
+class Counters(C.Structure):
+    _fields_ = [("ingress", C.c_uint64), ("egress", C.c_uint64),
+                ("handled", C.c_uint64), ("dropped", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+class FlowEntry(C.Structure):
+    _fields_ = [("tuple", C.c_uint8 * KEY_BYTES), ("pkts", C.c_uint64),
+                ("bytes", C.c_uint64), ("first_seen", C.c_uint64)]
+
+
+assert C.sizeof(Cfg) == 8 and C.sizeof(Frames) == 48
+assert C.sizeof(Counters) == 32 and C.sizeof(FlowEntry) == 64
+
+# every symbol declared in include/tcbee_amd.h, with its ctypes signature
+_SIGS = {
+    "tcbee_abi_version": (C.c_int, []),
+    "tcbee_strerror": (C.c_char_p, [C.c_int]),
+    "tcbee_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "tcbee_ctx_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_uint64,
+                                   C.c_uint64, C.c_uint64]),
+    "tcbee_ctx_destroy": (C.c_int, [C.c_void_p]),
+    "tcbee_ctx_stream": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
+    "tcbee_ctx_sync": (C.c_int, [C.c_void_p]),
+    "tcbee_parse_batch_device": (C.c_int, [C.c_void_p, C.POINTER(Frames), C.POINTER(Cfg),
+                                           C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.c_void_p]),
+    "tcbee_parse_batch": (C.c_int, [C.c_void_p, C.POINTER(Frames), C.POINTER(Cfg),
+                                    C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                    C.POINTER(C.c_uint64), C.POINTER(Counters)]),
+    "tcbee_flow_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "tcbee_flow_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64,
+                                    C.POINTER(C.c_uint64)]),
+    "tcbee_flow_reset": (C.c_int, [C.c_void_p]),
+    "tcbee_ctx_status": (C.c_int, [C.c_void_p]),
+    "tcbee_ctx_profile": (C.c_int, [C.c_void_p, C.c_int]),
+    "tcbee_ctx_profile_read": (C.c_int, [C.c_void_p, C.POINTER(C.c_double),
+                                         C.POINTER(C.c_uint64)]),
+    "tcbee_gen_frames_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                          C.c_uint64, C.c_int, C.c_uint64, C.c_uint64,
+                                          C.c_void_p]),
+    "tcbee_gen_frames_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                        C.c_uint64, C.c_int, C.c_uint64, C.c_uint64]),
+    "tcbee_flow_hash64": (C.c_uint64, [C.c_void_p]),
+}
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """The loaded libtcbee_amd.so. Raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `make -C tcbee_amd/csrc` "
+                "or __graft_entry__.build() (no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _strerror(code: int) -> str:
+    try:
+        return lib().tcbee_strerror(code).decode()
+    except Exception:  # library absent while formatting an error
+        return f"tcbee error {code}"
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != OK:
+        raise TcbeeError(rc, what)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(lib().tcbee_device_count(C.byref(n)), "tcbee_device_count")
+    return n.value

@@ -1,0 +1,454 @@
+// tcbee_capi.hip — the C ABI (include/tcbee_amd.h) over the HIP kernels.
+// No exceptions cross this boundary; every entry point returns a TCBEE_* code.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/tcbee_amd.h"
+#include "tcbee_gen.h"
+#include "tcbee_internal.h"
+#include "tcbee_layout.h"
+
+using namespace tcbee;
+
+struct tcbee_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint64_t max_frames = 0, max_arena = 0, max_flows = 0;
+  int fpl = 2;
+
+  FlowTable tab{};
+  uint64_t nslots = 0;
+  PersistState* d_persist = nullptr;
+  BatchState* d_batch = nullptr;
+  uint64_t* d_tile_status = nullptr;
+  uint64_t max_tiles = 0;
+  uint64_t* d_new_list = nullptr;
+  uint32_t* d_bitmap = nullptr;
+  uint32_t* d_wprefix = nullptr;
+  uint32_t* d_bprefix = nullptr;
+  uint32_t* d_slot_scratch = nullptr;
+  uint64_t max_words = 0, max_sblocks = 0;
+
+  // host-pointer path staging (allocated on first use)
+  uint8_t* d_arena = nullptr;
+  uint64_t* d_off = nullptr;
+  uint32_t* d_len = nullptr;
+  uint64_t* d_ts = nullptr;
+  uint8_t* d_rec = nullptr;
+  uint32_t* d_hash = nullptr;
+  uint32_t* d_id = nullptr;
+  uint64_t* d_n = nullptr;
+  tcbee_counters* d_ctr = nullptr;
+
+  // K1 timing (tcbee_ctx_profile)
+  bool profiling = false;
+  std::vector<hipEvent_t> ev;  // pairs
+  uint64_t ev_used = 0;
+};
+static constexpr uint64_t kMaxProfiled = 4096;
+
+namespace {
+
+int map_err(hipError_t e) {
+  if (e == hipSuccess) return TCBEE_OK;
+  if (e == hipErrorOutOfMemory) return TCBEE_ENOMEM;
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return TCBEE_ENODEV;
+  return TCBEE_EDEVICE;
+}
+
+#define TRY_HIP(expr)                          \
+  do {                                         \
+    hipError_t e_ = (expr);                    \
+    if (e_ != hipSuccess) return map_err(e_);  \
+  } while (0)
+
+template <class T>
+hipError_t dalloc(T** p, uint64_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  return hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+}
+
+void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+uint64_t tile_frames(int fpl) { return (uint64_t)kBlock * (uint64_t)fpl; }
+
+int ensure_host_path(tcbee_ctx* c) {
+  if (c->d_arena) return TCBEE_OK;
+  TRY_HIP(dalloc(&c->d_arena, c->max_arena + 16));
+  TRY_HIP(dalloc(&c->d_off, c->max_frames));
+  TRY_HIP(dalloc(&c->d_len, c->max_frames));
+  TRY_HIP(dalloc(&c->d_ts, c->max_frames));
+  TRY_HIP(dalloc(&c->d_rec, c->max_frames * kRecBytes + 16));
+  TRY_HIP(dalloc(&c->d_hash, c->max_frames));
+  TRY_HIP(dalloc(&c->d_id, c->max_frames));
+  TRY_HIP(dalloc(&c->d_n, 1));
+  TRY_HIP(dalloc(&c->d_ctr, 1));
+  return TCBEE_OK;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int tcbee_abi_version(void) { return TCBEE_ABI_VERSION; }
+
+const char* tcbee_strerror(int code) {
+  switch (code) {
+    case TCBEE_OK: return "ok";
+    case TCBEE_EINVAL: return "invalid argument";
+    case TCBEE_ENOMEM: return "out of memory";
+    case TCBEE_EDEVICE: return "HIP device error";
+    case TCBEE_ECAPACITY: return "batch exceeds context capacity";
+    case TCBEE_EFLOWFULL: return "flow table full";
+    case TCBEE_ENODEV: return "no HIP device";
+    case TCBEE_EIO: return "I/O error";
+    case TCBEE_EFORMAT: return "malformed input";
+    case TCBEE_ESPIN: return "in-kernel wait timed out";
+    default: return "unknown error";
+  }
+}
+
+int tcbee_device_count(int* n) {
+  if (!n) return TCBEE_EINVAL;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *n = c;
+  return TCBEE_OK;
+}
+
+int tcbee_ctx_destroy(tcbee_ctx* c) {
+  if (!c) return TCBEE_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  dfree(c->tab.meta);
+  dfree(c->tab.cnt);
+  dfree(c->d_persist);
+  dfree(c->d_batch);
+  dfree(c->d_tile_status);
+  dfree(c->d_new_list);
+  dfree(c->d_bitmap);
+  dfree(c->d_wprefix);
+  dfree(c->d_bprefix);
+  dfree(c->d_slot_scratch);
+  dfree(c->d_arena);
+  dfree(c->d_off);
+  dfree(c->d_len);
+  dfree(c->d_ts);
+  dfree(c->d_rec);
+  dfree(c->d_hash);
+  dfree(c->d_id);
+  dfree(c->d_n);
+  dfree(c->d_ctr);
+  for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return TCBEE_OK;
+}
+
+int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t max_arena,
+                     uint64_t max_flows) {
+  if (!out || max_frames == 0 || max_frames > (1ull << 40)) return TCBEE_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return TCBEE_ENODEV;
+  if (device < 0 || device >= ndev) return TCBEE_EINVAL;
+  tcbee_ctx* c = new (std::nothrow) tcbee_ctx();
+  if (!c) return TCBEE_ENOMEM;
+  c->device = device;
+  c->max_frames = max_frames;
+  c->max_arena = max_arena;
+  c->max_flows = max_flows < 16 ? 16 : max_flows;
+  if (const char* e = std::getenv("TCBEE_FPL")) {
+    const int v = std::atoi(e);
+    if (v == 1 || v == 2 || v == 4) c->fpl = v;
+  }
+  int rc = TCBEE_OK;
+  auto fail = [&](int code) {
+    tcbee_ctx_destroy(c);
+    return code;
+  };
+  if (hipSetDevice(device) != hipSuccess) return fail(TCBEE_EDEVICE);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(TCBEE_EDEVICE);
+  c->nslots = 64;
+  while (c->nslots < 2 * c->max_flows) c->nslots <<= 1;
+  c->tab.mask = c->nslots - 1;
+  c->max_tiles = (max_frames + tile_frames(1) - 1) / tile_frames(1);
+  c->max_words = (max_frames + 31) / 32;
+  c->max_sblocks = (c->max_words + kScanWordsPerBlock - 1) / kScanWordsPerBlock;
+  hipError_t e = hipSuccess;
+  if ((e = dalloc(&c->tab.meta, 8 * c->nslots)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->tab.cnt, 2 * c->nslots)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->d_persist, 1)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->d_batch, 1)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->d_tile_status, c->max_tiles)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->d_new_list, c->nslots)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->d_bitmap, c->max_words)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->d_wprefix, c->max_words)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->d_bprefix, c->max_sblocks)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->d_slot_scratch, max_frames)) != hipSuccess) return fail(map_err(e));
+  rc = tcbee_flow_reset(c);
+  if (rc != TCBEE_OK) return fail(rc);
+  *out = c;
+  return TCBEE_OK;
+}
+
+int tcbee_ctx_stream(tcbee_ctx* c, void** stream) {
+  if (!c || !stream) return TCBEE_EINVAL;
+  *stream = (void*)c->stream;
+  return TCBEE_OK;
+}
+
+int tcbee_ctx_sync(tcbee_ctx* c) {
+  if (!c) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  TRY_HIP(hipStreamSynchronize(c->stream));
+  return TCBEE_OK;
+}
+
+int tcbee_flow_reset(tcbee_ctx* c) {
+  if (!c) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  TRY_HIP(launch_table_init(c->tab, c->stream));
+  TRY_HIP(hipMemsetAsync(c->d_persist, 0, sizeof(PersistState), c->stream));
+  TRY_HIP(hipStreamSynchronize(c->stream));
+  return TCBEE_OK;
+}
+
+int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_cfg* cfg,
+                             uint8_t* out_rec74, uint64_t out_cap, uint32_t* out_flow_hash,
+                             uint32_t* out_flow_id, uint64_t* out_n_dev, tcbee_counters* ctr_dev,
+                             void* stream) {
+  if (!c || !in || !cfg) return TCBEE_EINVAL;
+  if (cfg->direction > 1) return TCBEE_EINVAL;
+  if (in->n > c->max_frames) return TCBEE_ECAPACITY;
+  if (in->n && (!in->arena || !in->offset || !in->caplen || !in->ts_ns)) return TCBEE_EINVAL;
+  if (out_cap && !out_rec74) return TCBEE_EINVAL;
+  if ((in->arena && !aligned16(in->arena)) || (out_rec74 && !aligned16(out_rec74)))
+    return TCBEE_EINVAL;
+  const bool flows = (cfg->flags & TCBEE_F_NO_FLOWS) == 0;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  TRY_HIP(hipSetDevice(c->device));
+  TRY_HIP(hipMemsetAsync(c->d_batch, 0, sizeof(BatchState), s));
+
+  const int fpl = c->fpl;
+  const uint64_t ntiles = (in->n + tile_frames(fpl) - 1) / tile_frames(fpl);
+  if (ntiles > 0) {
+    TRY_HIP(hipMemsetAsync(c->d_tile_status, 0, ntiles * sizeof(uint64_t), s));
+    ParseArgs a{};
+    a.arena = in->arena;
+    a.arena_len = in->arena_len;
+    a.offset = in->offset;
+    a.caplen = in->caplen;
+    a.ts = in->ts_ns;
+    a.n = in->n;
+    a.out_rec = out_rec74;
+    a.out_cap = out_cap;
+    a.out_hash = flows ? out_flow_hash : nullptr;
+    a.out_slot = out_flow_id ? out_flow_id : c->d_slot_scratch;
+    a.tile_status = c->d_tile_status;
+    a.ntiles = ntiles;
+    a.batch = c->d_batch;
+    a.persist = c->d_persist;
+    a.new_list = c->d_new_list;
+    a.tab = c->tab;
+    a.filter_port = cfg->filter_port;
+    const bool timed = c->profiling && c->ev_used < kMaxProfiled;
+    if (timed) TRY_HIP(hipEventRecord(c->ev[2 * c->ev_used], s));
+    TRY_HIP(launch_parse(a, fpl, flows, s));
+    if (timed) {
+      TRY_HIP(hipEventRecord(c->ev[2 * c->ev_used + 1], s));
+      ++c->ev_used;
+    }
+  }
+  if (flows && ntiles > 0) {
+    RankArgs r{};
+    r.new_list = c->d_new_list;
+    r.batch = c->d_batch;
+    r.persist = c->d_persist;
+    r.tab = c->tab;
+    r.bitmap = c->d_bitmap;
+    r.wprefix = c->d_wprefix;
+    r.bprefix = c->d_bprefix;
+    r.nwords = (in->n + 31) / 32;
+    r.nblocks = (r.nwords + kScanWordsPerBlock - 1) / kScanWordsPerBlock;
+    TRY_HIP(hipMemsetAsync(c->d_bitmap, 0, r.nwords * sizeof(uint32_t), s));
+    TRY_HIP(launch_rank(r, s));
+    if (out_flow_id) TRY_HIP(launch_gather_ids(out_flow_id, out_cap, c->d_batch, c->tab, s));
+  }
+  TRY_HIP(launch_finalize(c->d_batch, c->d_persist, out_cap, out_n_dev, ctr_dev, cfg->direction, s));
+  return TCBEE_OK;
+}
+
+int tcbee_parse_batch(tcbee_ctx* c, const tcbee_frames* in, const tcbee_cfg* cfg,
+                      uint8_t* out_rec74, uint64_t out_cap, uint32_t* out_flow_hash,
+                      uint32_t* out_flow_id, uint64_t* out_n, tcbee_counters* ctr) {
+  if (!c || !in || !cfg || !out_n) return TCBEE_EINVAL;
+  if (in->n > c->max_frames) return TCBEE_ECAPACITY;
+  if (in->arena_len > c->max_arena) return TCBEE_ECAPACITY;
+  if (in->n && (!in->arena || !in->offset || !in->caplen || !in->ts_ns)) return TCBEE_EINVAL;
+  if (out_cap && !out_rec74) return TCBEE_EINVAL;
+  int rc = ensure_host_path(c);
+  if (rc) return rc;
+  TRY_HIP(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const uint64_t n = in->n;
+  if (n) {
+    TRY_HIP(hipMemcpyAsync(c->d_arena, in->arena, in->arena_len, hipMemcpyHostToDevice, s));
+    TRY_HIP(hipMemcpyAsync(c->d_off, in->offset, n * 8, hipMemcpyHostToDevice, s));
+    TRY_HIP(hipMemcpyAsync(c->d_len, in->caplen, n * 4, hipMemcpyHostToDevice, s));
+    TRY_HIP(hipMemcpyAsync(c->d_ts, in->ts_ns, n * 8, hipMemcpyHostToDevice, s));
+  }
+  TRY_HIP(hipMemsetAsync(c->d_ctr, 0, sizeof(tcbee_counters), s));
+  tcbee_frames din{c->d_arena, in->arena_len, c->d_off, c->d_len, c->d_ts, n};
+  const uint64_t cap = out_cap < n ? out_cap : n;
+  rc = tcbee_parse_batch_device(c, &din, cfg, c->d_rec, cap, out_flow_hash ? c->d_hash : nullptr,
+                                out_flow_id ? c->d_id : nullptr, c->d_n, c->d_ctr, s);
+  if (rc) return rc;
+  uint64_t nout = 0;
+  tcbee_counters hc{};
+  TRY_HIP(hipMemcpyAsync(&nout, c->d_n, 8, hipMemcpyDeviceToHost, s));
+  TRY_HIP(hipMemcpyAsync(&hc, c->d_ctr, sizeof(hc), hipMemcpyDeviceToHost, s));
+  TRY_HIP(hipStreamSynchronize(s));
+  if (nout) {
+    TRY_HIP(hipMemcpyAsync(out_rec74, c->d_rec, nout * kRecBytes, hipMemcpyDeviceToHost, s));
+    if (out_flow_hash)
+      TRY_HIP(hipMemcpyAsync(out_flow_hash, c->d_hash, nout * 4, hipMemcpyDeviceToHost, s));
+    if (out_flow_id)
+      TRY_HIP(hipMemcpyAsync(out_flow_id, c->d_id, nout * 4, hipMemcpyDeviceToHost, s));
+    TRY_HIP(hipStreamSynchronize(s));
+  }
+  *out_n = nout;
+  if (ctr) {
+    ctr->ingress += hc.ingress;
+    ctr->egress += hc.egress;
+    ctr->handled += hc.handled;
+    ctr->dropped += hc.dropped;
+  }
+  return TCBEE_OK;
+}
+
+int tcbee_flow_count(tcbee_ctx* c, uint64_t* n) {
+  if (!c || !n) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  PersistState p{};
+  TRY_HIP(hipMemcpyAsync(&p, c->d_persist, sizeof(p), hipMemcpyDeviceToHost, c->stream));
+  TRY_HIP(hipStreamSynchronize(c->stream));
+  *n = p.flow_count;
+  return TCBEE_OK;
+}
+
+int tcbee_flow_export(tcbee_ctx* c, tcbee_flow_entry* out, uint64_t cap, uint64_t* n) {
+  if (!c || !n || (cap && !out)) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  std::vector<uint64_t> meta, cnt;
+  try {
+    meta.resize(8 * c->nslots);
+    cnt.resize(2 * c->nslots);
+  } catch (...) {
+    return TCBEE_ENOMEM;
+  }
+  PersistState p{};
+  TRY_HIP(hipMemcpyAsync(&p, c->d_persist, sizeof(p), hipMemcpyDeviceToHost, c->stream));
+  TRY_HIP(hipMemcpyAsync(meta.data(), c->tab.meta, meta.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  TRY_HIP(hipMemcpyAsync(cnt.data(), c->tab.cnt, cnt.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  TRY_HIP(hipStreamSynchronize(c->stream));
+  uint64_t written = 0;
+  for (uint64_t s = 0; s < c->nslots; ++s) {
+    const uint64_t* m = &meta[8 * s];
+    if (m[0] < 2 || m[7] == 0) continue;
+    const uint64_t id = m[7] - 1;
+    if (id >= cap) continue;
+    tcbee_flow_entry& e = out[id];
+    std::memcpy(e.tuple, m + 1, TCBEE_KEY_BYTES);
+    e.pkts = cnt[2 * s];
+    e.bytes = cnt[2 * s + 1];
+    e.first_seen = m[6];
+    ++written;
+  }
+  *n = p.flow_count < cap ? p.flow_count : cap;
+  (void)written;
+  return TCBEE_OK;
+}
+
+int tcbee_ctx_status(tcbee_ctx* c) {
+  if (!c) return TCBEE_EINVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return TCBEE_EDEVICE;
+  PersistState p{};
+  if (hipMemcpyAsync(&p, c->d_persist, sizeof(p), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return TCBEE_EDEVICE;
+  const uint32_t zero = 0;
+  if (hipMemcpyAsync(&c->d_persist->status, &zero, 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return TCBEE_EDEVICE;
+  if (p.status & kStSpin) return TCBEE_ESPIN;
+  if (p.status & kStFlowFull) return TCBEE_EFLOWFULL;
+  return TCBEE_OK;
+}
+
+int tcbee_ctx_profile(tcbee_ctx* c, int enable) {
+  if (!c) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  if (enable && c->ev.empty()) {
+    c->ev.resize(2 * kMaxProfiled, nullptr);
+    for (auto& e : c->ev) TRY_HIP(hipEventCreate(&e));
+  }
+  c->profiling = enable != 0;
+  c->ev_used = 0;
+  return TCBEE_OK;
+}
+
+int tcbee_ctx_profile_read(tcbee_ctx* c, double* ms_total, uint64_t* launches) {
+  if (!c || !ms_total || !launches) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  double tot = 0.0;
+  for (uint64_t k = 0; k < c->ev_used; ++k) {
+    TRY_HIP(hipEventSynchronize(c->ev[2 * k + 1]));
+    float ms = 0.f;
+    TRY_HIP(hipEventElapsedTime(&ms, c->ev[2 * k], c->ev[2 * k + 1]));
+    tot += ms;
+  }
+  *ms_total = tot;
+  *launches = c->ev_used;
+  return TCBEE_OK;
+}
+
+int tcbee_gen_frames_device(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
+                            uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed,
+                            void* stream) {
+  if ((n && (!arena || !off || !len)) || (kind != 0 && kind != 1)) return TCBEE_EINVAL;
+  if (kind == 1 && n_flows == 0) return TCBEE_EINVAL;
+  if (!n) return TCBEE_OK;
+  TRY_HIP(launch_gen(arena, off, len, n, first_index, kind, n_flows, seed, (hipStream_t)stream));
+  return TCBEE_OK;
+}
+
+int tcbee_gen_frames_host(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
+                          uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed) {
+  if ((n && (!arena || !off || !len)) || (kind != 0 && kind != 1)) return TCBEE_EINVAL;
+  if (kind == 1 && n_flows == 0) return TCBEE_EINVAL;
+  for (uint64_t i = 0; i < n; ++i) {
+    uint8_t h[54];
+    gen_header(h, first_index + i, len[i], kind, n_flows, seed);
+    std::memcpy(arena + off[i], h, len[i] < 54u ? len[i] : 54u);
+  }
+  return TCBEE_OK;
+}
+
+uint64_t tcbee_flow_hash64(const uint8_t key[TCBEE_KEY_BYTES]) {
+  uint64_t k[5];
+  std::memcpy(k, key, 40);
+  return flow_hash64(k[0], k[1], k[2], k[3], k[4]);
+}
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+// tcbee_gen.h — synthetic trace frames (DESIGN.md "Synthetic traces").
+// The same inline function builds the 54 header bytes of frame i on the host
+// and on the device, so device-generated traces are bit-identical to the
+// host-generated ones the parity tests feed the oracle. Payload bytes are zero.
+#pragma once
+#include "tcbee_layout.h"
+
+namespace tcbee {
+
+enum GenKind : int { kGenSingleFlow = 0, kGenMultiFlow = 1 };
+
+struct GenFields {
+  uint32_t saddr, daddr;  // numeric (a.b.c.d = a<<24 ...)
+  uint16_t sport, dport, window, check, ip_id;
+  uint32_t seq, ack;
+  uint8_t flags;
+};
+
+TCBEE_HD GenFields gen_fields(uint64_t i, int kind, uint64_t n_flows, uint64_t seed) {
+  GenFields g;
+  if (kind == kGenSingleFlow) {
+    // config 2 of BASELINE.json / SURVEY.md §8(d)
+    g.saddr = 0x0A000001u;  // 10.0.0.1
+    g.daddr = 0x0A000002u;  // 10.0.0.2
+    g.sport = 40000;
+    g.dport = 5201;
+    g.seq = (uint32_t)(1000u + 10u * (uint32_t)i);
+    g.ack = 1;
+    g.flags = 0x18;
+    g.window = 502;
+    g.check = (uint16_t)(((uint32_t)i * 2654435761u) >> 16);
+  } else {
+    const uint64_t r = splitmix64(seed + 0x1000ULL + i);
+    const uint64_t f = n_flows ? r % n_flows : 0;
+    const uint64_t fh = splitmix64((seed << 1) ^ (0xF10F10000000ULL + f));
+    g.saddr = 0x0A000000u | (uint32_t)(fh & 0xFFFFFFu);
+    g.daddr = 0xAC100000u | (uint32_t)((fh >> 24) & 0xFFFFFu);
+    g.sport = (uint16_t)(1024u + (uint32_t)((fh >> 44) % 64000u));
+    const uint16_t ports[4] = {80, 443, 5201, 8080};
+    g.dport = ports[(fh >> 62) & 3u];
+    g.seq = (uint32_t)(r >> 32);
+    g.ack = (uint32_t)splitmix64(r);
+    g.flags = 0x10;
+    g.window = (uint16_t)(256u + (uint32_t)((fh >> 8) % 65000u));
+    g.check = (uint16_t)(r >> 16);
+  }
+  g.ip_id = (uint16_t)i;
+  return g;
+}
+
+// Writes the 54 header bytes (eth + IPv4 + TCP, IHL 5, doff 5) of a frame of
+// `caplen` bytes.
+TCBEE_HD void gen_header(uint8_t* h, uint64_t i, uint32_t caplen, int kind, uint64_t n_flows,
+                         uint64_t seed) {
+  const GenFields g = gen_fields(i, kind, n_flows, seed);
+  // ethernet: dst 02:00:00:00:00:02, src 02:00:00:00:00:01, type IPv4
+  h[0] = 0x02; h[1] = 0; h[2] = 0; h[3] = 0; h[4] = 0; h[5] = 0x02;
+  h[6] = 0x02; h[7] = 0; h[8] = 0; h[9] = 0; h[10] = 0; h[11] = 0x01;
+  h[12] = 0x08; h[13] = 0x00;
+  uint8_t* ip = h + 14;
+  const uint32_t tot = caplen > 14 ? caplen - 14 : 0;
+  ip[0] = 0x45; ip[1] = 0;
+  ip[2] = (uint8_t)(tot >> 8); ip[3] = (uint8_t)tot;
+  ip[4] = (uint8_t)(g.ip_id >> 8); ip[5] = (uint8_t)g.ip_id;
+  ip[6] = 0x40; ip[7] = 0;  // DF
+  ip[8] = 64; ip[9] = kTcpProtocol;
+  ip[10] = 0; ip[11] = 0;
+  ip[12] = (uint8_t)(g.saddr >> 24); ip[13] = (uint8_t)(g.saddr >> 16);
+  ip[14] = (uint8_t)(g.saddr >> 8); ip[15] = (uint8_t)g.saddr;
+  ip[16] = (uint8_t)(g.daddr >> 24); ip[17] = (uint8_t)(g.daddr >> 16);
+  ip[18] = (uint8_t)(g.daddr >> 8); ip[19] = (uint8_t)g.daddr;
+  uint32_t sum = 0;
+  for (int k = 0; k < 20; k += 2) sum += ((uint32_t)ip[k] << 8) | ip[k + 1];
+  while (sum >> 16) sum = (sum & 0xFFFF) + (sum >> 16);
+  const uint16_t csum = (uint16_t)~sum;
+  ip[10] = (uint8_t)(csum >> 8); ip[11] = (uint8_t)csum;
+  uint8_t* t = h + 34;
+  t[0] = (uint8_t)(g.sport >> 8); t[1] = (uint8_t)g.sport;
+  t[2] = (uint8_t)(g.dport >> 8); t[3] = (uint8_t)g.dport;
+  t[4] = (uint8_t)(g.seq >> 24); t[5] = (uint8_t)(g.seq >> 16);
+  t[6] = (uint8_t)(g.seq >> 8); t[7] = (uint8_t)g.seq;
+  t[8] = (uint8_t)(g.ack >> 24); t[9] = (uint8_t)(g.ack >> 16);
+  t[10] = (uint8_t)(g.ack >> 8); t[11] = (uint8_t)g.ack;
+  t[12] = 0x50; t[13] = g.flags;
+  t[14] = (uint8_t)(g.window >> 8); t[15] = (uint8_t)g.window;
+  t[16] = (uint8_t)(g.check >> 8); t[17] = (uint8_t)g.check;
+  t[18] = 0; t[19] = 0;
+}
+
+}  // namespace tcbee

@@ -1,0 +1,93 @@
+// tcbee_internal.h — device-side state shared by the kernels and the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tcbee_amd.h"
+
+namespace tcbee {
+
+// Status bits (sticky, in PersistState::status)
+constexpr uint32_t kStFlowFull = 1u, kStSpin = 2u;
+
+// Flow table in HBM, open addressing, linear probing, power-of-two slots.
+//  meta[s*8 + 0] tag   (0 empty, 1 busy, else hash_tag(h))
+//  meta[s*8 + 1..5]    the 40-B key as 5 LE u64 words
+//  meta[s*8 + 6]       first_seen (global accepted-frame index, ~0 = none)
+//  meta[s*8 + 7]       dense flow id + 1 (0 = not yet assigned)
+//  cnt [s*2 + 0/1]     pkts / bytes (kept off the meta line: their atomics
+//                      would otherwise evict the key line from L2)
+struct FlowTable {
+  uint64_t* meta;
+  uint64_t* cnt;
+  uint64_t mask;  // slots - 1
+};
+
+// Lives across batches of one context.
+struct PersistState {
+  uint64_t rec_base;    // accepted frames before this batch
+  uint64_t flow_count;  // flows with ids
+  uint32_t status;
+  uint32_t pad0;
+  uint64_t pad1;
+};
+
+// Zeroed before every batch (one 32-B memset).
+struct BatchState {
+  uint64_t n_acc;   // accepted frames in this batch (last tile writes it)
+  uint64_t n_new;   // flows first claimed in this batch
+  uint32_t ticket;  // dynamic tile ticket
+  uint32_t pad0;
+  uint64_t pad1;
+};
+static_assert(sizeof(BatchState) == 32, "memset size");
+
+struct ParseArgs {
+  const uint8_t* arena;
+  uint64_t arena_len;
+  const uint64_t* offset;
+  const uint32_t* caplen;
+  const uint64_t* ts;
+  uint64_t n;
+  uint8_t* out_rec;
+  uint64_t out_cap;
+  uint32_t* out_hash;
+  uint32_t* out_slot;     // per record: flow-table slot (rewritten to ids later)
+  uint64_t* tile_status;  // decoupled look-back words, one per tile
+  uint64_t ntiles;
+  BatchState* batch;
+  PersistState* persist;
+  uint64_t* new_list;     // slots first claimed this batch
+  FlowTable tab;
+  uint16_t filter_port;
+};
+
+struct RankArgs {
+  const uint64_t* new_list;
+  BatchState* batch;
+  PersistState* persist;
+  FlowTable tab;
+  uint32_t* bitmap;     // one bit per accepted frame of the batch
+  uint32_t* wprefix;    // per bitmap word: exclusive popcount prefix in its block
+  uint32_t* bprefix;    // per scan block: exclusive popcount prefix
+  uint64_t nwords;
+  uint64_t nblocks;
+};
+
+// Launchers (tcbee_kernels.hip). All asynchronous on `s`.
+hipError_t launch_table_init(FlowTable t, hipStream_t s);
+hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s);
+hipError_t launch_rank(const RankArgs& r, hipStream_t s);
+hipError_t launch_gather_ids(uint32_t* ids, uint64_t cap, const BatchState* b,
+                             FlowTable t, hipStream_t s);
+hipError_t launch_finalize(BatchState* b, PersistState* p, uint64_t out_cap,
+                           uint64_t* out_n, tcbee_counters* ctr, int direction,
+                           hipStream_t s);
+hipError_t launch_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
+                      uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed,
+                      hipStream_t s);
+
+constexpr int kBlock = 256;
+constexpr int kScanWordsPerBlock = 2048;  // 256 threads x 8 words
+
+}  // namespace tcbee

@@ -1,0 +1,657 @@
+// tcbee_kernels.hip — HIP kernels (gfx950) of the packet-record path.
+//
+//   K1 k_parse     one lane per frame: bounds/ethertype/proto/port checks,
+//                  fixed-offset header extraction, the 74-B record, the flow
+//                  key + hash + flow-table upsert, and ORDER-PRESERVING
+//                  compaction of the records (decoupled look-back over dynamic
+//                  tiles), records staged in LDS and stored as 16-B vectors.
+//                  Restates xdp_hook / tc_hook (tcbee-ebpf/src/probes/xdp.rs:
+//                  27-223, tc.rs:28-183) + FLOWS insert (flow_tracker.rs:17-23)
+//                  + the drain task's serializer (tcbee/src/handlers/mod.rs:
+//                  104-139).
+//   K2 k_mark / k_scan_words / k_scan_blocks / k_assign
+//                  dense flow ids in first-seen order (the order in which
+//                  tcbee-process creates flows, db_writer.rs:51-65): a bitmap
+//                  over this batch's accepted frames marks each new flow's first
+//                  frame; id = popcount prefix.
+//   K3 k_gather    per record: slot -> dense id.
+//   k_finalize     counters (counters.rs) + record count + running bases.
+#include <hip/hip_runtime.h>
+
+#include "tcbee_gen.h"
+#include "tcbee_internal.h"
+#include "tcbee_layout.h"
+
+namespace tcbee {
+
+// ---------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Read at the coherence point (an RMW is never served from a stale cache).
+__device__ __forceinline__ uint64_t ld_coherent(uint64_t* p) {
+  return __hip_atomic_fetch_or(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
+__device__ __forceinline__ uint32_t bswap16(uint32_t v) {
+  return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu);
+}
+// bytes [r, r+4) of the 8-byte little-endian pair (lo, hi)
+__device__ __forceinline__ uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32_t r) {
+  return __builtin_amdgcn_alignbyte(hi, lo, r);
+}
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const uint32_t lane = __lane_id();
+  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+constexpr uint32_t kSpinLimit = 1u << 24;
+
+// 16 bytes at arena[a .. a+16), zero past arena_len (a is 16-B aligned).
+__device__ __forceinline__ uint4 load_chunk(const uint8_t* arena, uint64_t arena_len, uint64_t a) {
+  if (a + 16 <= arena_len) return *reinterpret_cast<const uint4*>(arena + a);
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int b = 0; b < 16; ++b)
+    if (a + b < arena_len) w[b >> 2] |= (uint32_t)arena[a + b] << (8 * (b & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// ---------------------------------------------------------------------------
+// The per-frame hook. Returns accept; fills the record as 19 dwords (bytes
+// 0..75, of which 74 are the record; dword 18 = 0x0000FFFF) and the 40-B key.
+// Accept set (identical for xdp_hook and tc_hook):
+//   caplen >= 14 && ethertype in {0x0800, 0x86DD} &&
+//   (v4: caplen >= 54 && ip[9] == 6  |  v6: caplen >= 74 && ip6[6] == 6) &&
+//   (filter_port == 0 || sport == filter_port || dport == filter_port)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool parse_frame(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                            uint64_t off, uint32_t caplen, uint64_t ts,
+                                            uint32_t filter_port, uint32_t (&R)[19],
+                                            uint64_t (&K)[5]) {
+  // clamp to the arena: a frame never extends past arena_len
+  if (off >= arena_len) caplen = 0;
+  else if (caplen > arena_len - off) caplen = (uint32_t)(arena_len - off);
+  if (caplen < kEthHdrLen) return false;  // xdp.rs:37-39
+
+  // Load the header window: 16-B aligned chunks covering [off, off+min(len,74)).
+  const uint64_t abase = off & ~15ull;
+  const uint32_t s = (uint32_t)(off & 15u);
+  const uint32_t need = s + (caplen < 74u ? caplen : 74u);
+  uint32_t w[24];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if ((uint32_t)(16 * c) < need) v = load_chunk(arena, arena_len, abase + 16u * c);
+    w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+  }
+  // Normalise so that u[j] holds frame bytes [4j, 4j+4): shift by s bytes
+  // (dword shift by s>>2 via two select stages, then a byte align by s&3).
+  // (bit masks, not ?: — hipcc turns a select cascade over an array into a
+  //  runtime-indexed scratch copy)
+  const uint32_t q = s >> 2, r = s & 3u;
+  const uint32_t m1 = 0u - (q & 1u), m2 = 0u - ((q >> 1) & 1u);
+  uint32_t t[23];
+#pragma unroll
+  for (int j = 0; j < 23; ++j) t[j] = (w[j] & ~m1) | (w[j + 1] & m1);
+  uint32_t v2[21];
+#pragma unroll
+  for (int j = 0; j < 21; ++j) v2[j] = (t[j] & ~m2) | (t[j + 2] & m2);
+  uint32_t u[19];
+#pragma unroll
+  for (int j = 0; j < 19; ++j) u[j] = align_bytes(v2[j + 1], v2[j], r);
+
+  const uint32_t ethertype = bswap16(u[3] & 0xFFFFu);  // bytes 12..13, xdp.rs:49
+  const bool v4 = ethertype == kEthertypeIPv4;
+  const bool v6 = ethertype == kEthertypeIPv6;
+  if (!v4 && !v6) return false;                               // xdp.rs:52
+  const uint32_t proto = v4 ? (u[5] >> 24) : (u[5] & 0xFFu);  // ip[9] @23 | ip6[6] @20
+  if (proto != kTcpProtocol) return false;                    // xdp.rs:73, :147
+  if (caplen < (v4 ? kV4MinLen : kV6MinLen)) return false;    // xdp.rs:60,78 / :134,152
+
+  // TCP header at frame byte 34 (v4) or 54 (v6): both are 2 mod 4.
+  uint32_t T[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) T[j] = v4 ? u[8 + j] : u[13 + j];
+  const uint32_t sport = bswap16(T[0] >> 16);                 // tcp[0..1]
+  const uint32_t dport = bswap16(T[1] & 0xFFFFu);             // tcp[2..3]
+  if (filter_port != 0 && sport != filter_port && dport != filter_port)
+    return false;                                              // xdp.rs:89-92
+  const uint32_t seq = bswap32(align_bytes(T[2], T[1], 2));   // tcp[4..7]
+  const uint32_t ack = bswap32(align_bytes(T[3], T[2], 2));   // tcp[8..11]
+  const uint32_t flagbits = T[3] >> 16;                       // tcp[12..13]
+  const uint32_t window = bswap16(T[4] & 0xFFFFu);            // tcp[14..15]
+  const uint32_t check = bswap16(T[4] >> 16);                 // tcp[16..17]
+  // `tcp_hdr.urg().to_be() == 1` (xdp.rs:105-110): bit -> u16 0/1 -> to_be()
+  // (0 or 0x0100 on little endian) == 1  => always false. Kept literal.
+  auto flag = [&](int index) -> uint32_t {
+    const uint32_t bit = (flagbits >> index) & 1u;  // bindgen bit `index` of bytes 12..13
+    return bswap16(bit) == 1u ? 1u : 0u;
+  };
+  const uint32_t f_urg = flag(13), f_ack = flag(12), f_psh = flag(11), f_rst = flag(10),
+                 f_syn = flag(9), f_fin = flag(8);
+
+  // addresses
+  const uint32_t sa4 = align_bytes(u[7], u[6], 2);  // wire bytes 26..29 as LE word
+  const uint32_t da4 = align_bytes(u[8], u[7], 2);  // 30..33
+  uint32_t sa6[4], da6[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sa6[j] = align_bytes(u[6 + j], u[5 + j], 2);    // 22..37
+    da6[j] = align_bytes(u[10 + j], u[9 + j], 2);   // 38..53
+  }
+
+  // record (tcp_packet_trace bincode + marker), xdp.rs:94-112 / :168-186
+  R[0] = (uint32_t)ts;
+  R[1] = (uint32_t)(ts >> 32);
+  R[2] = v4 ? bswap32(sa4) : 0u;  // saddr.to_be()
+  R[3] = v4 ? bswap32(da4) : 0u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    R[4 + j] = v6 ? sa6[j] : 0u;
+    R[8 + j] = v6 ? da6[j] : 0u;
+  }
+  R[12] = sport | (dport << 16);
+  R[13] = seq;
+  R[14] = ack;
+  R[15] = window | (f_urg << 16) | (f_ack << 24);
+  R[16] = f_psh | (f_rst << 8) | (f_syn << 16) | (f_fin << 24);
+  R[17] = check | 0xFFFF0000u;  // checksum + first half of FF FF FF FF
+  R[18] = 0x0000FFFFu;
+
+  // IpTuple key (xdp.rs:116-127 / :189-195): v4 address = 12 zero bytes + wire bytes
+  if (v4) {
+    K[0] = 0;
+    K[1] = (uint64_t)sa4 << 32;
+    K[2] = 0;
+    K[3] = (uint64_t)da4 << 32;
+  } else {
+    K[0] = (uint64_t)sa6[0] | ((uint64_t)sa6[1] << 32);
+    K[1] = (uint64_t)sa6[2] | ((uint64_t)sa6[3] << 32);
+    K[2] = (uint64_t)da6[0] | ((uint64_t)da6[1] << 32);
+    K[3] = (uint64_t)da6[2] | ((uint64_t)da6[3] << 32);
+  }
+  K[4] = (uint64_t)sport | ((uint64_t)dport << 16) | ((uint64_t)kTcpProtocol << 32);
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// Flow-table upsert. Identity = full 40-B key; the 64-bit tag only filters.
+// Claim protocol: CAS tag empty->busy, key words by agent-scope stores, drain,
+// then the tag (agent-scope store). Readers poll the tag relaxed (agent) and
+// read the key by agent-scope loads; a mismatch is re-checked at the coherence
+// point before the probe moves on (never a duplicate flow).
+// ---------------------------------------------------------------------------
+__device__ uint32_t flow_upsert(const FlowTable& T, const uint64_t (&K)[5], uint64_t h,
+                                BatchState* batch, uint64_t* new_list, PersistState* persist,
+                                uint64_t& fs_seen) {
+  const uint64_t tag = hash_tag(h);
+  uint64_t s = h & T.mask;
+  for (uint64_t probe = 0; probe <= T.mask; ++probe) {
+    uint64_t* m = T.meta + s * 8;
+    uint64_t cur = ld_agent(m);
+    if (cur == kTagEmpty) {
+      uint64_t expected = kTagEmpty;
+      if (__hip_atomic_compare_exchange_strong(m, &expected, kTagBusy, __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) st_agent(m + 1 + j, K[j]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st_agent(m, tag);
+        const uint64_t slot_no = atomicAdd((unsigned long long*)&batch->n_new, 1ull);
+        new_list[slot_no] = s;
+        fs_seen = ~0ull;
+        return (uint32_t)s;
+      }
+      cur = expected;
+    }
+    for (uint32_t spins = 0; cur == kTagBusy; ++spins) {
+      if (spins > kSpinLimit) {
+        atomicOr(&persist->status, kStSpin);
+        return 0xFFFFFFFFu;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      cur = ld_agent(m);
+    }
+    if (cur == tag) {
+      bool eq = true;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) eq = eq && (ld_agent(m + 1 + j) == K[j]);
+      if (!eq) {
+        eq = true;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) eq = eq && (ld_coherent(m + 1 + j) == K[j]);
+      }
+      if (eq) {
+        fs_seen = ld_agent(m + 6);
+        return (uint32_t)s;
+      }
+    }
+    s = (s + 1) & T.mask;
+  }
+  atomicOr(&persist->status, kStFlowFull);
+  return 0xFFFFFFFFu;
+}
+
+// ---------------------------------------------------------------------------
+// Decoupled look-back (one wave). Status word: bits 63:62 = 1 aggregate,
+// 2 inclusive prefix; bits 61:0 = value. Words are single 8-B agent-scope
+// stores polled by agent-scope loads (the data IS the flag).
+// ---------------------------------------------------------------------------
+constexpr uint64_t kFlagAgg = 1ull << 62, kFlagInc = 2ull << 62, kValMask = (1ull << 62) - 1;
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ uint64_t lookback(uint64_t* status, uint64_t tile, uint64_t count, PersistState* persist) {
+  const uint32_t lane = __lane_id();
+  if (tile == 0) {
+    if (lane == 0) st_agent(status, kFlagInc | count);
+    return 0;
+  }
+  if (lane == 0) st_agent(status + tile, kFlagAgg | count);
+  uint64_t excl = 0;
+  int64_t base = (int64_t)tile - 1;
+  for (;;) {
+    const int64_t idx = base - (int64_t)lane;
+    uint64_t v = idx >= 0 ? ld_agent(status + idx) : kFlagInc;
+    uint32_t spins = 0;
+    while (__any((v >> 62) == 0)) {
+      if (++spins > kSpinLimit) {
+        if (lane == 0) atomicOr(&persist->status, kStSpin);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      if ((v >> 62) == 0) v = ld_agent(status + idx);
+    }
+    const uint64_t inc = __ballot((v >> 62) == 2);
+    if (inc) {
+      const uint32_t first = (uint32_t)__ffsll((unsigned long long)inc) - 1;
+      excl += wave_sum64(lane <= first ? (v & kValMask) : 0ull);
+      break;
+    }
+    excl += wave_sum64(v & kValMask);
+    base -= 64;
+  }
+  if (lane == 0) st_agent(status + tile, kFlagInc | (excl + count));
+  return excl;
+}
+
+// record -> LDS at byte offset `bo` (even)
+__device__ __forceinline__ void lds_put_record(uint32_t* srec, uint32_t bo, const uint32_t (&R)[19]) {
+  uint16_t* s16 = reinterpret_cast<uint16_t*>(srec);
+  if ((bo & 3u) == 0) {
+    const uint32_t d = bo >> 2;
+#pragma unroll
+    for (int j = 0; j < 18; ++j) srec[d + j] = R[j];
+    s16[(bo + 72) >> 1] = (uint16_t)R[18];
+  } else {
+    s16[bo >> 1] = (uint16_t)R[0];
+    const uint32_t d = (bo + 2) >> 2;
+#pragma unroll
+    for (int j = 0; j < 18; ++j) srec[d + j] = (R[j] >> 16) | (R[j + 1] << 16);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K1
+// ---------------------------------------------------------------------------
+template <int FPL, bool FLOWS>
+__global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
+  constexpr int TILE = kBlock * FPL;
+  constexpr int SREC_DW = (TILE * kRecBytes + 32) / 4;
+  __shared__ __attribute__((aligned(16))) uint32_t s_rec[SREC_DW];
+  __shared__ uint32_t s_wcnt[FPL][4];
+  __shared__ uint64_t s_tile, s_excl;
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  if (tid == 0) s_tile = atomicAdd(&a.batch->ticket, 1u);
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  const uint64_t i0 = tile * (uint64_t)TILE;
+  const uint64_t rec_base = a.persist->rec_base;
+
+  uint32_t R[FPL][19];
+  bool acc[FPL];
+  uint32_t rank[FPL], slot[FPL], hsh[FPL], clen[FPL];
+  uint64_t fs_seen[FPL];
+
+#pragma unroll
+  for (int f = 0; f < FPL; ++f) {
+    const uint64_t i = i0 + (uint64_t)f * kBlock + tid;
+    acc[f] = false;
+    slot[f] = 0xFFFFFFFFu;
+    hsh[f] = 0;
+    clen[f] = 0;
+    fs_seen[f] = ~0ull;
+    uint64_t K[5] = {0, 0, 0, 0, 0};
+    if (i < a.n) {
+      const uint64_t off = a.offset[i];
+      clen[f] = a.caplen[i];
+      const uint64_t ts = a.ts[i];
+      acc[f] = parse_frame(a.arena, a.arena_len, off, clen[f], ts, a.filter_port, R[f], K);
+    }
+    if (FLOWS) {
+      const uint64_t am = __ballot(acc[f]);
+      if (am) {
+        // wave-uniform key (one flow in the whole wave): one lane probes
+        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)am) - 1;
+        bool same = true;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) same = same && (!acc[f] || K[j] == __shfl(K[j], leader));
+        const uint64_t h = flow_hash64(K[0], K[1], K[2], K[3], K[4]);
+        if (acc[f]) hsh[f] = fold32(h);
+        if (__all(same)) {
+          uint32_t sl = 0xFFFFFFFFu;
+          uint64_t fs = ~0ull;
+          if (lane == leader) sl = flow_upsert(a.tab, K, h, a.batch, a.new_list, a.persist, fs);
+          slot[f] = __shfl(sl, leader);
+          fs_seen[f] = __shfl(fs, leader);
+        } else if (acc[f]) {
+          slot[f] = flow_upsert(a.tab, K, h, a.batch, a.new_list, a.persist, fs_seen[f]);
+        }
+      }
+    }
+    const uint64_t b = __ballot(acc[f]);
+    if (lane == 0) s_wcnt[f][wave] = (uint32_t)__popcll(b);
+    rank[f] = (uint32_t)__popcll(b & lanemask_lt());
+  }
+  __syncthreads();
+  uint32_t running = 0;
+#pragma unroll
+  for (int f = 0; f < FPL; ++f) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t c = s_wcnt[f][w];
+      if ((uint32_t)w == wave) rank[f] += running;
+      running += c;
+    }
+  }
+  const uint32_t total = running;
+#pragma unroll
+  for (int f = 0; f < FPL; ++f)
+    if (acc[f]) lds_put_record(s_rec, rank[f] * kRecBytes, R[f]);
+
+  if (wave == 0) {
+    const uint64_t excl = lookback(a.tile_status, tile, total, a.persist);
+    if (lane == 0) s_excl = excl;
+  }
+  __syncthreads();
+  const uint64_t excl = s_excl;
+  if (tid == 0 && tile == a.ntiles - 1) a.batch->n_acc = excl + total;
+
+  // ---- records: LDS -> HBM, 16-B stores, partial chunks as 2-B stores ----
+  const uint64_t wr_lo = excl < a.out_cap ? excl : a.out_cap;
+  const uint64_t wr_hi = (excl + total) < a.out_cap ? (excl + total) : a.out_cap;
+  if (wr_hi > wr_lo) {
+    const uint64_t G0 = wr_lo * kRecBytes, G1 = wr_hi * kRecBytes;
+    const uint64_t A = G0 & ~15ull;
+    const uint32_t head = (uint32_t)(G0 & 15u);
+    const uint32_t nchunks = (uint32_t)((G1 - A + 15) >> 4);
+    const uint16_t* s16 = reinterpret_cast<const uint16_t*>(s_rec);
+    for (uint32_t c = tid; c < nchunks; c += kBlock) {
+      const uint64_t g = A + 16ull * c;
+      if (g >= G0 && g + 16 <= G1) {
+        const uint32_t sb = 16u * c - head;
+        const uint32_t d0 = sb >> 2;
+        uint4 o;
+        if ((sb & 3u) == 0) {
+          o = make_uint4(s_rec[d0], s_rec[d0 + 1], s_rec[d0 + 2], s_rec[d0 + 3]);
+        } else {
+          const uint32_t x0 = s_rec[d0], x1 = s_rec[d0 + 1], x2 = s_rec[d0 + 2],
+                         x3 = s_rec[d0 + 3], x4 = s_rec[d0 + 4];
+          o = make_uint4((x0 >> 16) | (x1 << 16), (x1 >> 16) | (x2 << 16),
+                         (x2 >> 16) | (x3 << 16), (x3 >> 16) | (x4 << 16));
+        }
+        *reinterpret_cast<uint4*>(a.out_rec + g) = o;
+      } else {
+        const uint64_t lo = g > G0 ? g : G0;
+        const uint64_t hi = (g + 16) < G1 ? (g + 16) : G1;
+        for (uint64_t b = lo; b < hi; b += 2)
+          *reinterpret_cast<uint16_t*>(a.out_rec + b) = s16[(b - G0) >> 1];
+      }
+    }
+  }
+
+  // ---- per-record side outputs + flow counters ----
+#pragma unroll
+  for (int f = 0; f < FPL; ++f) {
+    const uint64_t p = excl + rank[f];
+    if (acc[f] && p < a.out_cap) {
+      if (a.out_hash) a.out_hash[p] = hsh[f];
+      if (FLOWS) a.out_slot[p] = slot[f];
+    }
+    if (FLOWS) {
+      const uint64_t am = __ballot(acc[f] && slot[f] != 0xFFFFFFFFu);
+      if (am) {
+        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)am) - 1;
+        const uint32_t s0 = __shfl(slot[f], leader);
+        const bool mine = acc[f] && slot[f] != 0xFFFFFFFFu;
+        if (__all(!mine || slot[f] == s0)) {
+          const uint64_t bsum = wave_sum64(mine ? (uint64_t)clen[f] : 0ull);
+          if (lane == leader) {
+            atomicAdd((unsigned long long*)&a.tab.cnt[2ull * s0], (unsigned long long)__popcll(am));
+            atomicAdd((unsigned long long*)&a.tab.cnt[2ull * s0 + 1], (unsigned long long)bsum);
+            const uint64_t gidx = rec_base + p;  // leader = lowest rank in the wave
+            if (gidx < fs_seen[f])
+              atomicMin((unsigned long long*)&a.tab.meta[8ull * s0 + 6], (unsigned long long)gidx);
+          }
+        } else if (mine) {
+          const uint64_t s = slot[f];
+          atomicAdd((unsigned long long*)&a.tab.cnt[2 * s], 1ull);
+          atomicAdd((unsigned long long*)&a.tab.cnt[2 * s + 1], (unsigned long long)clen[f]);
+          const uint64_t gidx = rec_base + p;
+          if (gidx < fs_seen[f])
+            atomicMin((unsigned long long*)&a.tab.meta[8 * s + 6], (unsigned long long)gidx);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// flow table init: tags/keys/ids 0, first_seen ~0, counters 0
+// ---------------------------------------------------------------------------
+__global__ void k_table_init(FlowTable t) {
+  const uint64_t nslots = t.mask + 1;
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < nslots;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t* m = t.meta + 8 * s;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = 0;
+    m[6] = ~0ull;
+    t.cnt[2 * s] = 0;
+    t.cnt[2 * s + 1] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K2: ranks of this batch's new flows by first_seen
+// ---------------------------------------------------------------------------
+__global__ void k_mark(RankArgs r) {
+  const uint64_t n_new = r.batch->n_new;
+  const uint64_t base = r.persist->rec_base;
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n_new;
+       j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t s = r.new_list[j];
+    const uint64_t local = r.tab.meta[8 * s + 6] - base;
+    atomicOr(&r.bitmap[local >> 5], 1u << (local & 31));
+  }
+}
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp, uint32_t& total) {
+  // 256 threads, 4 waves
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) s_tmp[wave] = x;
+  __syncthreads();
+  uint32_t wbase = 0;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    if ((uint32_t)w < wave) wbase += s_tmp[w];
+    total += s_tmp[w];
+  }
+  __syncthreads();
+  return wbase + x - v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_words(RankArgs r) {
+  __shared__ uint32_t s_tmp[4];
+  const uint64_t w0 = (uint64_t)blockIdx.x * kScanWordsPerBlock + threadIdx.x * 8ull;
+  uint32_t c[8], sum = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    c[k] = (w0 + k < r.nwords) ? (uint32_t)__popc(r.bitmap[w0 + k]) : 0u;
+    sum += c[k];
+  }
+  uint32_t total;
+  uint32_t pre = block_excl_scan(sum, s_tmp, total);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (w0 + k < r.nwords) r.wprefix[w0 + k] = pre;
+    pre += c[k];
+  }
+  if (threadIdx.x == 0) r.bprefix[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_blocks(RankArgs r) {
+  __shared__ uint32_t s_tmp[4];
+  uint32_t carry = 0;
+  for (uint64_t b0 = 0; b0 < r.nblocks; b0 += kBlock) {
+    const uint64_t b = b0 + threadIdx.x;
+    const uint32_t v = b < r.nblocks ? r.bprefix[b] : 0u;
+    uint32_t total;
+    const uint32_t pre = block_excl_scan(v, s_tmp, total);
+    if (b < r.nblocks) r.bprefix[b] = carry + pre;
+    carry += total;
+  }
+}
+
+__global__ void k_assign(RankArgs r) {
+  const uint64_t n_new = r.batch->n_new;
+  const uint64_t base = r.persist->rec_base;
+  const uint64_t fbase = r.persist->flow_count;
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n_new;
+       j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t s = r.new_list[j];
+    const uint64_t local = r.tab.meta[8 * s + 6] - base;
+    const uint64_t w = local >> 5;
+    const uint32_t below = r.bitmap[w] & ((1u << (local & 31)) - 1u);
+    const uint64_t id = fbase + r.bprefix[w / kScanWordsPerBlock] + r.wprefix[w] + __popc(below);
+    r.tab.meta[8 * s + 7] = id + 1;
+  }
+}
+
+// K3: slot -> dense id, in place
+__global__ void k_gather(uint32_t* ids, uint64_t cap, const BatchState* b, FlowTable t) {
+  const uint64_t n = b->n_acc < cap ? b->n_acc : cap;
+  for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < n;
+       p += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t s = ids[p];
+    ids[p] = s == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(t.meta[8ull * s + 7] - 1);
+  }
+}
+
+__global__ void k_finalize(BatchState* b, PersistState* p, uint64_t out_cap, uint64_t* out_n,
+                           tcbee_counters* ctr, int direction) {
+  const uint64_t n_acc = b->n_acc;
+  const uint64_t written = n_acc < out_cap ? n_acc : out_cap;
+  if (out_n) *out_n = written;
+  if (ctr) {
+    if (direction) ctr->egress += n_acc;  // EGRESS_EVENTS, tc.rs:167
+    else ctr->ingress += n_acc;           // INGRESS_EVENTS, xdp.rs:207
+    ctr->handled += written;              // EVENTS_HANDLED, xdp.rs:214
+    ctr->dropped += n_acc - written;      // EVENTS_DROPPED, xdp.rs:217
+  }
+  p->rec_base += n_acc;
+  p->flow_count += b->n_new;
+}
+
+// ---------------------------------------------------------------------------
+// synthetic trace headers (payload stays as the caller zeroed it)
+// ---------------------------------------------------------------------------
+__global__ void k_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
+                      uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    uint8_t h[54];
+    gen_header(h, first_index + i, len[i], kind, n_flows, seed);
+    const uint32_t m = len[i] < 54u ? len[i] : 54u;
+    uint8_t* dst = arena + off[i];
+    for (uint32_t b = 0; b < m; ++b) dst[b] = h[b];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+static unsigned grid_for(uint64_t n, unsigned cap = 4096) {
+  const uint64_t g = (n + kBlock - 1) / kBlock;
+  return (unsigned)(g == 0 ? 1 : (g > cap ? cap : g));
+}
+
+hipError_t launch_table_init(FlowTable t, hipStream_t s) {
+  hipLaunchKernelGGL(k_table_init, dim3(grid_for(t.mask + 1)), dim3(kBlock), 0, s, t);
+  return hipGetLastError();
+}
+
+template <int FPL>
+static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s) {
+  const dim3 grid((unsigned)a.ntiles);
+  if (flows) hipLaunchKernelGGL((k_parse<FPL, true>), grid, dim3(kBlock), 0, s, a);
+  else hipLaunchKernelGGL((k_parse<FPL, false>), grid, dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s) {
+  switch (fpl) {
+    case 1: return launch_parse_fpl<1>(a, flows, s);
+    case 2: return launch_parse_fpl<2>(a, flows, s);
+    case 4: return launch_parse_fpl<4>(a, flows, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_rank(const RankArgs& r, hipStream_t s) {
+  hipLaunchKernelGGL(k_mark, dim3(1024), dim3(kBlock), 0, s, r);
+  hipLaunchKernelGGL(k_scan_words, dim3((unsigned)r.nblocks), dim3(kBlock), 0, s, r);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, r);
+  hipLaunchKernelGGL(k_assign, dim3(1024), dim3(kBlock), 0, s, r);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_ids(uint32_t* ids, uint64_t cap, const BatchState* b, FlowTable t,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(k_gather, dim3(2048), dim3(kBlock), 0, s, ids, cap, b, t);
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize(BatchState* b, PersistState* p, uint64_t out_cap, uint64_t* out_n,
+                           tcbee_counters* ctr, int direction, hipStream_t s) {
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1), 0, s, b, p, out_cap, out_n, ctr, direction);
+  return hipGetLastError();
+}
+
+hipError_t launch_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
+                      uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_gen, dim3(grid_for(n, 8192)), dim3(kBlock), 0, s, arena, off, len, n,
+                     first_index, kind, n_flows, seed);
+  return hipGetLastError();
+}
+
+}  // namespace tcbee

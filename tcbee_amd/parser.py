@@ -1,0 +1,178 @@
+"""The packet-record path on an MI355X: a Python handle over ``tcbee_ctx``.
+
+One :class:`PacketParser` = one ``tcbee_ctx`` = one HIP stream and one flow
+table. It plays the role the reference gives to the attached XDP/TC programs
+(tcbee-record/tcbee-ebpf/src/main.rs:69-83) plus the drain task that
+serializes their ring entries (tcbee-record/tcbee/src/handlers/mod.rs:94-146):
+frames in, 74-byte ``*.tcp`` records out, in input order.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from .trace import Trace
+
+FLOW_DTYPE = np.dtype([("tuple", np.uint8, (40,)), ("pkts", np.uint64),
+                       ("bytes", np.uint64), ("first_seen", np.uint64)])
+assert FLOW_DTYPE.itemsize == 64
+
+
+@dataclass
+class ParseResult:
+    records: np.ndarray              # uint8 [n, 74]
+    flow_hash: np.ndarray | None     # uint32 [n]
+    flow_id: np.ndarray | None       # uint32 [n]
+    counters: dict = field(default_factory=dict)
+
+    @property
+    def n(self) -> int:
+        return len(self.records)
+
+    def tobytes(self) -> bytes:
+        """The bytes tcbee-record would have appended to xdp.tcp / tc.tcp."""
+        return self.records.tobytes()
+
+
+def _ptr(x) -> int:
+    """Raw address of a numpy array, torch tensor or int."""
+    if x is None:
+        return 0
+    if isinstance(x, int):
+        return x
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    if hasattr(x, "data_ptr"):
+        return int(x.data_ptr())
+    raise TypeError(type(x))
+
+
+class PacketParser:
+    def __init__(self, device: int = 0, max_frames: int = 1 << 20, max_arena: int = 0,
+                 max_flows: int = 1 << 16):
+        L = _lib.lib()
+        h = C.c_void_p()
+        _lib.check(L.tcbee_ctx_create(C.byref(h), device, C.c_uint64(max_frames),
+                                      C.c_uint64(max_arena), C.c_uint64(max_flows)),
+                   "tcbee_ctx_create")
+        self._h = h
+        self.device = device
+        self.max_frames = max_frames
+        self.max_arena = max_arena
+        self.max_flows = max_flows
+
+    # -- lifetime -----------------------------------------------------------
+    def close(self) -> None:
+        if self._h:
+            _lib.lib().tcbee_ctx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        s = C.c_void_p()
+        _lib.check(_lib.lib().tcbee_ctx_stream(self._h, C.byref(s)), "tcbee_ctx_stream")
+        return s.value or 0
+
+    def sync(self) -> None:
+        _lib.check(_lib.lib().tcbee_ctx_sync(self._h), "tcbee_ctx_sync")
+
+    def status(self) -> int:
+        """Sticky in-kernel status since the last call (OK / EFLOWFULL / ESPIN)."""
+        return _lib.lib().tcbee_ctx_status(self._h)
+
+    # -- host-pointer path ---------------------------------------------------
+    def parse(self, trace: Trace, filter_port: int = 0, direction: int = _lib.DIR_INGRESS,
+              flows: bool = True, out_cap: int | None = None) -> ParseResult:
+        """Synchronous: H2D frames, parse, D2H records (+ flow hash / id)."""
+        n = trace.n
+        cap = n if out_cap is None else int(out_cap)
+        rec = np.empty((max(cap, 1), _lib.RECORD_BYTES), dtype=np.uint8)
+        fh = np.empty(max(cap, 1), dtype=np.uint32) if flows else None
+        fi = np.empty(max(cap, 1), dtype=np.uint32) if flows else None
+        fr = _lib.Frames(trace.arena.ctypes.data if len(trace.arena) else 0, len(trace.arena),
+                         trace.offset.ctypes.data, trace.caplen.ctypes.data,
+                         trace.ts_ns.ctypes.data, n)
+        cfg = _lib.Cfg(filter_port, direction, 0, 0 if flows else _lib.F_NO_FLOWS)
+        nout = C.c_uint64(0)
+        ctr = _lib.Counters()
+        _lib.check(_lib.lib().tcbee_parse_batch(
+            self._h, C.byref(fr), C.byref(cfg), rec.ctypes.data, C.c_uint64(cap),
+            _ptr(fh), _ptr(fi), C.byref(nout), C.byref(ctr)), "tcbee_parse_batch")
+        k = nout.value
+        return ParseResult(rec[:k], fh[:k] if flows else None, fi[:k] if flows else None,
+                           ctr.as_dict())
+
+    # -- device-resident path -------------------------------------------------
+    def parse_device(self, arena, arena_len: int, offset, caplen, ts_ns, n: int,
+                     out_rec, out_cap: int, out_hash=None, out_id=None, out_n=None,
+                     counters=None, filter_port: int = 0,
+                     direction: int = _lib.DIR_INGRESS, flows: bool = True,
+                     stream: int | None = None) -> None:
+        """Asynchronous parse of frames already in HBM (pointers or torch tensors).
+
+        out_n: device u64[1]; counters: device u64[4] (accumulated)."""
+        fr = _lib.Frames(_ptr(arena), arena_len, _ptr(offset), _ptr(caplen), _ptr(ts_ns), n)
+        cfg = _lib.Cfg(filter_port, direction, 0, 0 if flows else _lib.F_NO_FLOWS)
+        _lib.check(_lib.lib().tcbee_parse_batch_device(
+            self._h, C.byref(fr), C.byref(cfg), _ptr(out_rec), C.c_uint64(out_cap),
+            _ptr(out_hash), _ptr(out_id), _ptr(out_n), _ptr(counters),
+            C.c_void_p(stream or 0)), "tcbee_parse_batch_device")
+
+    # -- measurement --------------------------------------------------------------
+    def profile(self, enable: bool = True) -> None:
+        _lib.check(_lib.lib().tcbee_ctx_profile(self._h, int(enable)), "tcbee_ctx_profile")
+
+    def profile_read(self):
+        """(summed K1 ms, K1 launches) since profile(True)."""
+        ms = C.c_double(0)
+        k = C.c_uint64(0)
+        _lib.check(_lib.lib().tcbee_ctx_profile_read(self._h, C.byref(ms), C.byref(k)),
+                   "tcbee_ctx_profile_read")
+        return ms.value, k.value
+
+    # -- flow table -------------------------------------------------------------
+    def flow_count(self) -> int:
+        n = C.c_uint64(0)
+        _lib.check(_lib.lib().tcbee_flow_count(self._h, C.byref(n)), "tcbee_flow_count")
+        return n.value
+
+    def flows(self) -> np.ndarray:
+        """Flow table in dense-id (first-seen) order, dtype FLOW_DTYPE."""
+        cnt = self.flow_count()
+        out = np.zeros(max(cnt, 1), dtype=FLOW_DTYPE)
+        n = C.c_uint64(0)
+        _lib.check(_lib.lib().tcbee_flow_export(self._h, out.ctypes.data, C.c_uint64(cnt),
+                                                C.byref(n)), "tcbee_flow_export")
+        return out[:n.value]
+
+    def reset_flows(self) -> None:
+        _lib.check(_lib.lib().tcbee_flow_reset(self._h), "tcbee_flow_reset")
+
+
+def gen_frames_device(arena, offset, caplen, n: int, kind: int, n_flows: int, seed: int,
+                      stream: int | None = None, first_index: int = 0) -> None:
+    """Device generator: header bytes of frames whose index is already in HBM."""
+    _lib.check(_lib.lib().tcbee_gen_frames_device(
+        _ptr(arena), _ptr(offset), _ptr(caplen), C.c_uint64(n), C.c_uint64(first_index), kind,
+        C.c_uint64(n_flows), C.c_uint64(seed), C.c_void_p(stream or 0)),
+        "tcbee_gen_frames_device")
+
+
+def flow_hash64(key40: bytes) -> int:
+    buf = (C.c_uint8 * 40).from_buffer_copy(bytes(key40))
+    return int(_lib.lib().tcbee_flow_hash64(buf))

@@ -1,0 +1,128 @@
+"""Frame traces: the input side of the path (a NIC ring / trace file replayed).
+
+A :class:`Trace` is the host view of ``tcbee_frames`` (include/tcbee_amd.h):
+frame ``i`` is ``arena[offset[i] : offset[i] + caplen[i]]`` with timestamp
+``ts_ns[i]`` (which stands in for ``bpf_ktime_get_ns()``,
+tcbee-ebpf/src/probes/xdp.rs:95).
+
+Synthetic traces follow BASELINE.json configs 2-4; the header
+bytes come from the library's generator (tcbee_amd/csrc/tcbee_gen.h) so the
+host and device versions of a trace are bit-identical.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+
+TS_BASE_NS = 1_000_000_000
+TS_STEP_NS = 1_000
+IMIX_SIZES = (64, 576, 1500)  # 7 : 4 : 1
+DEFAULT_SEED = 0x7CBEE
+
+GEN_SINGLE = 0
+GEN_MULTI = 1
+
+
+@dataclass
+class Trace:
+    arena: np.ndarray   # uint8
+    offset: np.ndarray  # uint64
+    caplen: np.ndarray  # uint32
+    ts_ns: np.ndarray   # uint64
+
+    def __post_init__(self):
+        self.arena = np.ascontiguousarray(self.arena, dtype=np.uint8)
+        self.offset = np.ascontiguousarray(self.offset, dtype=np.uint64)
+        self.caplen = np.ascontiguousarray(self.caplen, dtype=np.uint32)
+        self.ts_ns = np.ascontiguousarray(self.ts_ns, dtype=np.uint64)
+        n = len(self.offset)
+        if len(self.caplen) != n or len(self.ts_ns) != n:
+            raise ValueError("offset/caplen/ts_ns length mismatch")
+
+    @property
+    def n(self) -> int:
+        return len(self.offset)
+
+    def frame(self, i: int) -> bytes:
+        o = int(self.offset[i])
+        return self.arena[o:o + int(self.caplen[i])].tobytes()
+
+    def slice(self, lo: int, hi: int) -> "Trace":
+        """Frames [lo, hi) with a re-based, compact arena."""
+        off = self.offset[lo:hi]
+        ln = self.caplen[lo:hi]
+        if hi <= lo:
+            return Trace(np.zeros(0, np.uint8), off, ln, self.ts_ns[lo:hi])
+        a0 = int(off.min())
+        a1 = int((off + ln).max())
+        return Trace(self.arena[a0:a1].copy(), off - np.uint64(a0), ln.copy(),
+                     self.ts_ns[lo:hi].copy())
+
+    @staticmethod
+    def from_frames(frames, ts_ns=None) -> "Trace":
+        """Pack a list of byte strings back to back."""
+        lens = np.array([len(f) for f in frames], dtype=np.uint32)
+        off = np.zeros(len(frames), dtype=np.uint64)
+        if len(frames):
+            off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        arena = np.frombuffer(b"".join(frames), dtype=np.uint8).copy()
+        if ts_ns is None:
+            ts_ns = TS_BASE_NS + TS_STEP_NS * np.arange(len(frames), dtype=np.uint64)
+        return Trace(arena, off, lens, np.asarray(ts_ns, dtype=np.uint64))
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    """Vectorised splitmix64 (== tcbee::splitmix64 in tcbee_layout.h)."""
+    x = np.asarray(x, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def synth_index(n: int, sizes: str = "64", seed: int = DEFAULT_SEED, first_index: int = 0):
+    """offset/caplen/ts_ns of a synthetic trace and its arena length.
+
+    sizes="64": every frame 64 B (config 2); sizes="imix": 64/576/1500 at 7:4:1
+    drawn per frame from splitmix64(seed ^ 0x1M1X + i) % 12 (config 3/4).
+    Frames are packed back to back (no padding), as in a capture file.
+    """
+    i = np.arange(first_index, first_index + n, dtype=np.uint64)
+    if sizes == "64":
+        caplen = np.full(n, 64, dtype=np.uint32)
+    elif sizes == "imix":
+        r = splitmix64(np.uint64(seed ^ 0x1A1E) + i) % np.uint64(12)
+        caplen = np.where(r < 7, 64, np.where(r < 11, 576, 1500)).astype(np.uint32)
+    else:
+        raise ValueError(sizes)
+    offset = np.zeros(n, dtype=np.uint64)
+    if n:
+        np.cumsum(caplen[:-1], dtype=np.uint64, out=offset[1:])
+    ts = np.uint64(TS_BASE_NS) + np.uint64(TS_STEP_NS) * i
+    arena_len = int(offset[-1]) + int(caplen[-1]) if n else 0
+    return offset, caplen, ts, arena_len
+
+
+def gen_frames_host(arena: np.ndarray, offset: np.ndarray, caplen: np.ndarray,
+                    kind: int, n_flows: int, seed: int, first_index: int = 0) -> None:
+    """Writes the header bytes of every frame into ``arena`` (payload untouched)."""
+    rc = _lib.lib().tcbee_gen_frames_host(
+        arena.ctypes.data_as(C.c_void_p), offset.ctypes.data_as(C.c_void_p),
+        caplen.ctypes.data_as(C.c_void_p), C.c_uint64(len(offset)), C.c_uint64(first_index),
+        kind, C.c_uint64(n_flows), C.c_uint64(seed))
+    _lib.check(rc, "tcbee_gen_frames_host")
+
+
+def synth_trace(n: int, sizes: str = "64", kind: int = GEN_SINGLE, n_flows: int = 1,
+                seed: int = DEFAULT_SEED, first_index: int = 0) -> Trace:
+    """A synthetic trace on the host (configs 2/3 of BASELINE.json): global frames
+    [first_index, first_index + n), arena re-based to the first of them."""
+    offset, caplen, ts, arena_len = synth_index(n, sizes, seed, first_index)
+    arena = np.zeros(arena_len + 16, dtype=np.uint8)
+    gen_frames_host(arena, offset, caplen, kind, n_flows, seed, first_index)
+    return Trace(arena[:arena_len] if arena_len else arena[:0], offset, caplen, ts)

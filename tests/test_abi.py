@@ -1,0 +1,101 @@
+"""C-ABI library checks that need no GPU: it loads, exports exactly what
+include/tcbee_amd.h declares, and its host-side pieces agree with the oracle."""
+import os
+import re
+import struct
+
+import numpy as np
+import pytest
+
+import tcbee_amd
+from tcbee_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "tcbee_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(tcbee_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    L = tcbee_amd.lib()
+    declared = header_functions()
+    assert len(declared) >= 15
+    for name in declared:
+        assert hasattr(L, name), f"{name} declared in include/tcbee_amd.h but not exported"
+    assert sorted(_lib.EXPORTED) == declared
+
+
+def test_abi_version_and_errors():
+    L = tcbee_amd.lib()
+    assert L.tcbee_abi_version() == 1
+    assert L.tcbee_strerror(0) == b"ok"
+    assert L.tcbee_strerror(_lib.EFLOWFULL) == b"flow table full"
+
+
+def test_device_count_does_not_crash():
+    assert tcbee_amd.device_count() >= 0
+
+
+def test_ctx_create_fails_loudly_without_gpu():
+    if tcbee_amd.device_count() > 0:
+        pytest.skip("GPU present")
+    with pytest.raises(tcbee_amd.TcbeeError) as e:
+        tcbee_amd.PacketParser(max_frames=16)
+    assert e.value.code == _lib.ENODEV
+
+
+def test_flow_hash_matches_oracle(oracle):
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        k = bytes(rng.integers(0, 256, 40, dtype=np.uint8))
+        assert tcbee_amd.flow_hash64(k) == oracle.flow_hash64(k)
+
+
+def test_generator_config2_frame0():
+    tr = tcbee_amd.synth_trace(3, sizes="64")
+    f0 = tr.frame(0)
+    assert len(f0) == 64
+    assert f0[12:14] == b"\x08\x00" and f0[14] == 0x45 and f0[23] == 6
+    assert f0[26:30] == bytes([10, 0, 0, 1]) and f0[30:34] == bytes([10, 0, 0, 2])
+    sport, dport, seq, ack = struct.unpack("!HHII", f0[34:46])
+    assert (sport, dport, seq, ack) == (40000, 5201, 1000, 1)
+    assert f0[46:48] == b"\x50\x18"
+    assert struct.unpack("!H", f0[48:50])[0] == 502
+    f2 = tr.frame(2)
+    assert struct.unpack("!I", f2[38:42])[0] == 1020
+    assert struct.unpack("!H", f2[50:52])[0] == ((2 * 2654435761) & 0xFFFFFFFF) >> 16
+    assert f0[54:] == bytes(10)
+    # IPv4 header checksum verifies
+    s = sum(struct.unpack("!10H", f0[14:34]))
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    assert s == 0xFFFF
+
+
+def test_generator_records_through_oracle(oracle):
+    tr = tcbee_amd.synth_trace(1000, sizes="64")
+    rec, fh, fi, ctr, table = oracle.parse(tr)
+    assert len(rec) == 1000 and len(table) == 1 and int(table["pkts"][0]) == 1000
+    r = rec[7].tobytes()
+    assert struct.unpack("<Q", r[:8])[0] == 1_000_000_000 + 7000
+    assert struct.unpack("<I", r[52:56])[0] == 1070
+
+
+def test_imix_proportions():
+    off, ln, ts, alen = tcbee_amd.synth_index(120000, sizes="imix")
+    c = np.bincount(np.searchsorted([64, 576, 1500], ln))
+    frac = c / c.sum()
+    assert np.allclose(frac, [7 / 12, 4 / 12, 1 / 12], atol=0.01)
+    assert alen == int(ln.sum()) and int(off[-1]) + int(ln[-1]) == alen
+    assert np.all(np.diff(ts.astype(np.int64)) > 0)
+
+
+def test_multiflow_generator_flow_count(oracle):
+    tr = tcbee_amd.synth_trace(20000, sizes="imix", kind=1, n_flows=100)
+    rec, fh, fi, ctr, table = oracle.parse(tr)
+    assert len(rec) == 20000
+    assert len(table) == 100
+    assert int(table["bytes"].sum()) == int(tr.caplen.sum())

@@ -1,0 +1,195 @@
+"""HIP path vs the CPU oracle, through the C ABI. Integer/byte work: bit-exact.
+
+Every comparison covers the 74-B records, the per-record flow hash and dense
+flow id, the counters (counters.rs) and the exported flow table.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import tcbee_amd
+from tcbee_amd.trace import Trace
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+KAT = json.load(open(os.path.join(HERE, "golden", "kat_vectors.json")))["vectors"]
+
+
+def assert_same(gpu_res, orc_res, gpu_flows=None):
+    rec, fh, fi, ctr, table = orc_res
+    assert gpu_res.n == len(rec)
+    if len(rec):
+        bad = np.nonzero(np.any(gpu_res.records != rec, axis=1))[0]
+        assert len(bad) == 0, f"{len(bad)} records differ, first at {bad[:5]}: " \
+            f"gpu {gpu_res.records[bad[0]].tobytes().hex()} oracle {rec[bad[0]].tobytes().hex()}"
+    if gpu_res.flow_hash is not None:
+        assert np.array_equal(gpu_res.flow_hash, fh)
+        assert np.array_equal(gpu_res.flow_id, fi)
+    assert gpu_res.counters == ctr
+    if gpu_flows is not None and table is not None:
+        assert len(gpu_flows) == len(table)
+        assert np.array_equal(gpu_flows["tuple"], table["tuple"])
+        assert np.array_equal(gpu_flows["pkts"], table["pkts"])
+        assert np.array_equal(gpu_flows["bytes"], table["bytes"])
+        assert np.array_equal(gpu_flows["first_seen"], table["first_seen"])
+
+
+def test_kat_vectors_single_batch(parser, oracle):
+    for port in sorted({v["filter_port"] for v in KAT}):
+        vs = [v for v in KAT if v["filter_port"] == port]
+        tr = Trace.from_frames([bytes.fromhex(v["frame"]) for v in vs],
+                               ts_ns=[v["ts"] for v in vs])
+        parser.reset_flows()
+        res = parser.parse(tr, filter_port=port)
+        exp = [bytes.fromhex(v["expect"]) for v in vs if v["expect"]]
+        assert [r.tobytes() for r in res.records] == exp
+        assert_same(res, oracle.parse(tr, filter_port=port), parser.flows())
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 255, 256, 257, 511, 512, 513, 1023, 1025, 4099])
+def test_mixed_sizes(parser, oracle, n):
+    from tracegen import mixed_trace
+    tr = mixed_trace(n, seed=n)
+    parser.reset_flows()
+    assert_same(parser.parse(tr), oracle.parse(tr), parser.flows())
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("port", [0, 5201, 80])
+@pytest.mark.parametrize("direction", [0, 1])
+def test_mixed_large(parser, oracle, seed, port, direction):
+    from tracegen import mixed_trace
+    tr = mixed_trace(200_000, seed=seed, n_flows=3000)
+    parser.reset_flows()
+    res = parser.parse(tr, filter_port=port, direction=direction)
+    assert_same(res, oracle.parse(tr, filter_port=port, direction=direction), parser.flows())
+    assert parser.status() == 0
+
+
+def test_no_flows_flag(parser, oracle):
+    from tracegen import mixed_trace
+    tr = mixed_trace(50_000, seed=9)
+    parser.reset_flows()
+    res = parser.parse(tr, flows=False)
+    rec, _, _, ctr, _ = oracle.parse(tr, flows=False)
+    assert np.array_equal(res.records, rec) and res.counters == ctr
+    assert parser.flow_count() == 0
+
+
+@pytest.mark.parametrize("cap", [0, 1, 100, 777])
+def test_out_cap_drops(parser, oracle, cap):
+    from tracegen import mixed_trace
+    tr = mixed_trace(20_000, seed=4)
+    parser.reset_flows()
+    res = parser.parse(tr, out_cap=cap)
+    orc = oracle.parse(tr, out_cap=cap)
+    assert_same(res, orc, parser.flows())
+
+
+def test_multi_batch_flow_ids_continue(parser, oracle):
+    from tracegen import mixed_trace
+    tr = mixed_trace(60_000, seed=21, n_flows=500)
+    parser.reset_flows()
+    ft = oracle.new_flowtab()
+    base = 0
+    try:
+        for lo, hi in [(0, 10_000), (10_000, 10_000), (10_000, 33_333), (33_333, 60_000)]:
+            part = tr.slice(lo, hi)
+            res = parser.parse(part)
+            orc = oracle.parse(part, ft=ft, record_base=base)
+            assert_same(res, orc)
+            base += len(orc[0])
+        gf = parser.flows()
+        of = oracle.flows(ft)
+        assert np.array_equal(gf, of)
+    finally:
+        oracle.free_flowtab(ft)
+
+
+def test_empty_batch(parser, oracle):
+    parser.reset_flows()
+    tr = Trace(np.zeros(0, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32),
+               np.zeros(0, np.uint64))
+    res = parser.parse(tr)
+    assert res.n == 0 and res.counters == {"ingress": 0, "egress": 0, "handled": 0,
+                                           "dropped": 0}
+
+
+def test_config2_1M_bit_exact(parser, oracle):
+    tr = tcbee_amd.synth_trace(1_000_000, sizes="64")
+    parser.reset_flows()
+    res = parser.parse(tr)
+    orc = oracle.parse(tr)
+    assert_same(res, orc, parser.flows())
+    fl = parser.flows()
+    assert len(fl) == 1 and int(fl["pkts"][0]) == 1_000_000 and int(fl["first_seen"][0]) == 0
+
+
+def test_config3_imix_multiflow(parser, oracle):
+    tr = tcbee_amd.synth_trace(300_000, sizes="imix", kind=1, n_flows=10_000)
+    parser.reset_flows()
+    assert_same(parser.parse(tr), oracle.parse(tr), parser.flows())
+
+
+def test_device_generator_matches_host(gpu):
+    import torch
+    for sizes, kind, nf in [("64", 0, 1), ("imix", 1, 777)]:
+        n = 100_000
+        off, ln, ts, alen = tcbee_amd.synth_index(n, sizes=sizes)
+        host = tcbee_amd.synth_trace(n, sizes=sizes, kind=kind, n_flows=nf)
+        d_arena = torch.zeros(alen + 16, dtype=torch.uint8, device="cuda")
+        d_off = torch.from_numpy(off.view(np.int64)).cuda()
+        d_len = torch.from_numpy(ln.view(np.int32)).cuda()
+        tcbee_amd.gen_frames_device(d_arena, d_off, d_len, n, kind, nf, tcbee_amd.trace.DEFAULT_SEED)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_arena[:alen].cpu().numpy(), host.arena)
+
+
+def test_device_path_matches_host_path(parser, oracle):
+    """parse_device on torch-allocated HBM buffers == host path == oracle."""
+    import torch
+    from tracegen import mixed_trace
+    tr = mixed_trace(100_000, seed=33)
+    n = tr.n
+    d_arena = torch.from_numpy(tr.arena).cuda()
+    d_off = torch.from_numpy(tr.offset.view(np.int64)).cuda()
+    d_len = torch.from_numpy(tr.caplen.view(np.int32)).cuda()
+    d_ts = torch.from_numpy(tr.ts_ns.view(np.int64)).cuda()
+    d_rec = torch.empty(n * 74 + 16, dtype=torch.uint8, device="cuda")
+    d_hash = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_id = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_n = torch.zeros(1, dtype=torch.int64, device="cuda")
+    d_ctr = torch.zeros(4, dtype=torch.int64, device="cuda")
+    parser.reset_flows()
+    parser.parse_device(d_arena, len(tr.arena), d_off, d_len, d_ts, n, d_rec, n, d_hash, d_id,
+                        d_n, d_ctr)
+    parser.sync()
+    k = int(d_n.item())
+    rec, fh, fi, ctr, table = oracle.parse(tr)
+    assert k == len(rec)
+    assert np.array_equal(d_rec[: k * 74].cpu().numpy().reshape(k, 74), rec)
+    assert np.array_equal(d_hash[:k].cpu().numpy().view(np.uint32), fh)
+    assert np.array_equal(d_id[:k].cpu().numpy().view(np.uint32), fi)
+    c = d_ctr.cpu().numpy()
+    assert dict(zip(["ingress", "egress", "handled", "dropped"], map(int, c))) == ctr
+
+
+@pytest.mark.parametrize("fpl", ["1", "2", "4"])
+def test_tile_shape_determinism(gpu, oracle, fpl, monkeypatch):
+    """Same trace, different frames-per-lane tilings -> identical outputs."""
+    from tracegen import mixed_trace
+    monkeypatch.setenv("TCBEE_FPL", fpl)
+    tr = mixed_trace(150_000, seed=77, n_flows=2000)
+    with tcbee_amd.PacketParser(max_frames=1 << 18, max_arena=1 << 26, max_flows=1 << 14) as p:
+        assert_same(p.parse(tr), oracle.parse(tr), p.flows())
+
+
+def test_flow_table_full_reports(gpu):
+    from tracegen import mixed_trace
+    tr = mixed_trace(50_000, seed=5, n_flows=5000)
+    with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 25, max_flows=16) as p:
+        res = p.parse(tr)
+        assert res.n > 0
+        assert p.status() == tcbee_amd._lib.EFLOWFULL
