@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libtcbee_amd.so")
@@ -109,6 +110,7 @@ def lib() -> C.CDLL:
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with `make -C tcbee_amd/csrc` "
                 "or __graft_entry__.build() (no CPU fallback exists)")
+        _share_hip_runtime_with_torch()
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(L, name)
@@ -116,6 +118,19 @@ def lib() -> C.CDLL:
             f.argtypes = args
         _lib = L
     return _lib
+
+
+def _share_hip_runtime_with_torch() -> None:
+    """libtcbee_amd.so needs libamdhip64.so.7, and torch-ROCm bundles its own copy
+    under the same soname: only one can live in a process. If torch is installed,
+    load it first so both share torch's runtime (loading /opt/rocm's first makes
+    torch report "No HIP GPUs are available")."""
+    if "torch" in sys.modules or os.environ.get("TCBEE_NO_TORCH"):
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
 
 
 def _strerror(code: int) -> str:

@@ -31,6 +31,8 @@ struct tcbee_ctx {
   uint32_t* d_wprefix = nullptr;
   uint32_t* d_bprefix = nullptr;
   uint32_t* d_slot_scratch = nullptr;
+  uint32_t* d_len_scratch = nullptr;
+  int n_cu = 256;
   uint64_t max_words = 0, max_sblocks = 0;
 
   // host-pointer path staging (allocated on first use)
@@ -139,6 +141,7 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
   dfree(c->d_wprefix);
   dfree(c->d_bprefix);
   dfree(c->d_slot_scratch);
+  dfree(c->d_len_scratch);
   dfree(c->d_arena);
   dfree(c->d_off);
   dfree(c->d_len);
@@ -196,6 +199,10 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   if ((e = dalloc(&c->d_wprefix, c->max_words)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_bprefix, c->max_sblocks)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_slot_scratch, max_frames)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->d_len_scratch, max_frames)) != hipSuccess) return fail(map_err(e));
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    c->n_cu = prop.multiProcessorCount;
   rc = tcbee_flow_reset(c);
   if (rc != TCBEE_OK) return fail(rc);
   *out = c;
@@ -254,7 +261,8 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     a.out_rec = out_rec74;
     a.out_cap = out_cap;
     a.out_hash = flows ? out_flow_hash : nullptr;
-    a.out_slot = out_flow_id ? out_flow_id : c->d_slot_scratch;
+    a.acc_slot = c->d_slot_scratch;
+    a.acc_len = c->d_len_scratch;
     a.tile_status = c->d_tile_status;
     a.ntiles = ntiles;
     a.batch = c->d_batch;
@@ -283,7 +291,18 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     r.nblocks = (r.nwords + kScanWordsPerBlock - 1) / kScanWordsPerBlock;
     TRY_HIP(hipMemsetAsync(c->d_bitmap, 0, r.nwords * sizeof(uint32_t), s));
     TRY_HIP(launch_rank(r, s));
-    if (out_flow_id) TRY_HIP(launch_gather_ids(out_flow_id, out_cap, c->d_batch, c->tab, s));
+    CountArgs k{};
+    k.acc_slot = c->d_slot_scratch;
+    k.acc_len = c->d_len_scratch;
+    k.out_id = out_flow_id;
+    k.out_cap = out_cap;
+    k.batch = c->d_batch;
+    k.persist = c->d_persist;
+    k.meta = c->tab.meta;
+    k.cnt = c->tab.cnt;
+    const uint64_t want = (in->n + 16 * kCountBlock - 1) / (16 * kCountBlock);
+    const unsigned grid = (unsigned)(want < (uint64_t)c->n_cu ? (want ? want : 1) : c->n_cu);
+    TRY_HIP(launch_count(k, grid, s));
   }
   TRY_HIP(launch_finalize(c->d_batch, c->d_persist, out_cap, out_n_dev, ctr_dev, cfg->direction, s));
   return TCBEE_OK;
@@ -370,8 +389,8 @@ int tcbee_flow_export(tcbee_ctx* c, tcbee_flow_entry* out, uint64_t cap, uint64_
     if (id >= cap) continue;
     tcbee_flow_entry& e = out[id];
     std::memcpy(e.tuple, m + 1, TCBEE_KEY_BYTES);
-    e.pkts = cnt[2 * s];
-    e.bytes = cnt[2 * s + 1];
+    e.pkts = cnt[2 * id];
+    e.bytes = cnt[2 * id + 1];
     e.first_seen = m[6];
     ++written;
   }

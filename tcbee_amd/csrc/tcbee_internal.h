@@ -15,8 +15,8 @@ constexpr uint32_t kStFlowFull = 1u, kStSpin = 2u;
 //  meta[s*8 + 1..5]    the 40-B key as 5 LE u64 words
 //  meta[s*8 + 6]       first_seen (global accepted-frame index, ~0 = none)
 //  meta[s*8 + 7]       dense flow id + 1 (0 = not yet assigned)
-//  cnt [s*2 + 0/1]     pkts / bytes (kept off the meta line: their atomics
-//                      would otherwise evict the key line from L2)
+//  cnt [id*2 + 0/1]    pkts / bytes of dense flow id `id` (by id, not slot:
+//                      k_count histograms them per dense id)
 struct FlowTable {
   uint64_t* meta;
   uint64_t* cnt;
@@ -52,7 +52,8 @@ struct ParseArgs {
   uint8_t* out_rec;
   uint64_t out_cap;
   uint32_t* out_hash;
-  uint32_t* out_slot;     // per record: flow-table slot (rewritten to ids later)
+  uint32_t* acc_slot;     // per accepted frame: flow-table slot (ctx scratch)
+  uint32_t* acc_len;      // per accepted frame: caplen (ctx scratch)
   uint64_t* tile_status;  // decoupled look-back words, one per tile
   uint64_t ntiles;
   BatchState* batch;
@@ -78,8 +79,17 @@ struct RankArgs {
 hipError_t launch_table_init(FlowTable t, hipStream_t s);
 hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s);
 hipError_t launch_rank(const RankArgs& r, hipStream_t s);
-hipError_t launch_gather_ids(uint32_t* ids, uint64_t cap, const BatchState* b,
-                             FlowTable t, hipStream_t s);
+struct CountArgs {
+  const uint32_t* acc_slot;
+  const uint32_t* acc_len;
+  uint32_t* out_id;
+  uint64_t out_cap;
+  const BatchState* batch;
+  const PersistState* persist;
+  const uint64_t* meta;
+  uint64_t* cnt;
+};
+hipError_t launch_count(const CountArgs& c, unsigned grid, hipStream_t s);
 hipError_t launch_finalize(BatchState* b, PersistState* p, uint64_t out_cap,
                            uint64_t* out_n, tcbee_counters* ctr, int direction,
                            hipStream_t s);
@@ -89,5 +99,7 @@ hipError_t launch_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, 
 
 constexpr int kBlock = 256;
 constexpr int kScanWordsPerBlock = 2048;  // 256 threads x 8 words
+constexpr int kCountBlock = 1024;
+constexpr int kCountBins = 16384;         // 2 x 64 KiB of LDS
 
 }  // namespace tcbee

@@ -421,36 +421,32 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
     }
   }
 
-  // ---- per-record side outputs + flow counters ----
+  // ---- per-record side outputs; first_seen = min accepted index ----
+  // (pkts/bytes are NOT counted here: per-record memory-side atomics cost more
+  //  than the whole parse; k_count histograms them by dense id in LDS.)
 #pragma unroll
   for (int f = 0; f < FPL; ++f) {
     const uint64_t p = excl + rank[f];
-    if (acc[f] && p < a.out_cap) {
-      if (a.out_hash) a.out_hash[p] = hsh[f];
-      if (FLOWS) a.out_slot[p] = slot[f];
+    if (acc[f]) {
+      if (a.out_hash && p < a.out_cap) a.out_hash[p] = hsh[f];
+      if (FLOWS) {
+        a.acc_slot[p] = slot[f];
+        a.acc_len[p] = clen[f];
+      }
     }
     if (FLOWS) {
-      const uint64_t am = __ballot(acc[f] && slot[f] != 0xFFFFFFFFu);
+      const bool mine = acc[f] && slot[f] != 0xFFFFFFFFu;
+      const uint64_t am = __ballot(mine);
       if (am) {
         const uint32_t leader = (uint32_t)__ffsll((unsigned long long)am) - 1;
         const uint32_t s0 = __shfl(slot[f], leader);
-        const bool mine = acc[f] && slot[f] != 0xFFFFFFFFu;
+        const uint64_t gidx = rec_base + p;
         if (__all(!mine || slot[f] == s0)) {
-          const uint64_t bsum = wave_sum64(mine ? (uint64_t)clen[f] : 0ull);
-          if (lane == leader) {
-            atomicAdd((unsigned long long*)&a.tab.cnt[2ull * s0], (unsigned long long)__popcll(am));
-            atomicAdd((unsigned long long*)&a.tab.cnt[2ull * s0 + 1], (unsigned long long)bsum);
-            const uint64_t gidx = rec_base + p;  // leader = lowest rank in the wave
-            if (gidx < fs_seen[f])
-              atomicMin((unsigned long long*)&a.tab.meta[8ull * s0 + 6], (unsigned long long)gidx);
-          }
-        } else if (mine) {
-          const uint64_t s = slot[f];
-          atomicAdd((unsigned long long*)&a.tab.cnt[2 * s], 1ull);
-          atomicAdd((unsigned long long*)&a.tab.cnt[2 * s + 1], (unsigned long long)clen[f]);
-          const uint64_t gidx = rec_base + p;
-          if (gidx < fs_seen[f])
-            atomicMin((unsigned long long*)&a.tab.meta[8 * s + 6], (unsigned long long)gidx);
+          // leader = lowest rank of the wave = its smallest accepted index
+          if (lane == leader && gidx < fs_seen[f])
+            atomicMin((unsigned long long*)&a.tab.meta[8ull * s0 + 6], (unsigned long long)gidx);
+        } else if (mine && gidx < fs_seen[f]) {
+          atomicMin((unsigned long long*)&a.tab.meta[8ull * slot[f] + 6], (unsigned long long)gidx);
         }
       }
     }
@@ -468,7 +464,7 @@ __global__ void k_table_init(FlowTable t) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) m[j] = 0;
     m[6] = ~0ull;
-    t.cnt[2 * s] = 0;
+    t.cnt[2 * s] = 0;  // ids < slots: the by-id counters share the index range
     t.cnt[2 * s + 1] = 0;
   }
 }
@@ -556,14 +552,89 @@ __global__ void k_assign(RankArgs r) {
   }
 }
 
-// K3: slot -> dense id, in place
-__global__ void k_gather(uint32_t* ids, uint64_t cap, const BatchState* b, FlowTable t) {
-  const uint64_t n = b->n_acc < cap ? b->n_acc : cap;
-  for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < n;
-       p += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t s = ids[p];
-    ids[p] = s == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(t.meta[8ull * s + 7] - 1);
+// K3: per accepted frame, slot -> dense id (written for records p < out_cap) and
+// pkts/bytes per flow. While every flow fits the LDS bins (<= kCountBins), each
+// block histograms a contiguous range of accepted frames in LDS and flushes the
+// non-zero bins with one global atomic pair each; bins are u32 and a block
+// flushes before its running byte total could wrap one. Otherwise per-frame
+// global atomics (wave-uniform flows aggregated first).
+__global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
+  __shared__ uint32_t s_pk[kCountBins];
+  __shared__ uint32_t s_by[kCountBins];
+  __shared__ uint64_t s_red[kCountBlock / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint64_t n_acc = c.batch->n_acc;
+  const uint64_t nflows = c.persist->flow_count + c.batch->n_new;
+  const bool use_lds = nflows <= (uint64_t)kCountBins;
+  const uint64_t per = ((n_acc + gridDim.x - 1) / gridDim.x + kCountBlock - 1) / kCountBlock * kCountBlock;
+  const uint64_t lo = (uint64_t)blockIdx.x * per;
+  const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
+  if (use_lds) {
+    for (uint32_t b = tid; b < nflows; b += kCountBlock) s_pk[b] = s_by[b] = 0;
+    __syncthreads();
   }
+  auto flush = [&]() {
+    __syncthreads();
+    for (uint32_t b = tid; b < nflows; b += kCountBlock) {
+      const uint32_t pk = s_pk[b];
+      if (pk) {
+        atomicAdd((unsigned long long*)&c.cnt[2ull * b], (unsigned long long)pk);
+        atomicAdd((unsigned long long*)&c.cnt[2ull * b + 1], (unsigned long long)s_by[b]);
+        s_pk[b] = 0;
+        s_by[b] = 0;
+      }
+    }
+    __syncthreads();
+  };
+  uint64_t running = 0;  // bytes added to the bins since the last flush (block-uniform)
+  for (uint64_t base = lo; base < hi; base += kCountBlock) {
+    const uint64_t p = base + tid;
+    const bool valid = p < hi;
+    const uint32_t s = valid ? c.acc_slot[p] : 0xFFFFFFFFu;
+    const uint32_t len = valid ? c.acc_len[p] : 0u;
+    const uint32_t id = s == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(c.meta[8ull * s + 7] - 1);
+    if (c.out_id && valid && p < c.out_cap) c.out_id[p] = id;
+    const bool mine = id != 0xFFFFFFFFu;
+    const uint64_t am = __ballot(mine);
+    const uint32_t leader = am ? (uint32_t)__ffsll((unsigned long long)am) - 1 : 0u;
+    const uint32_t id0 = __shfl(id, leader);
+    const bool uniform = __all(!mine || id == id0);
+    if (!use_lds) {
+      if (uniform) {
+        const uint64_t bs = wave_sum64(mine ? (uint64_t)len : 0ull);
+        if (am && lane == leader) {
+          atomicAdd((unsigned long long*)&c.cnt[2ull * id0], (unsigned long long)__popcll(am));
+          atomicAdd((unsigned long long*)&c.cnt[2ull * id0 + 1], (unsigned long long)bs);
+        }
+      } else if (mine) {
+        atomicAdd((unsigned long long*)&c.cnt[2ull * id], 1ull);
+        atomicAdd((unsigned long long*)&c.cnt[2ull * id + 1], (unsigned long long)len);
+      }
+      continue;
+    }
+    const uint64_t ws = wave_sum64(mine ? (uint64_t)len : 0ull);
+    if (lane == 0) s_red[wave] = ws;
+    __syncthreads();
+    uint64_t chunk = 0;
+#pragma unroll
+    for (int w = 0; w < kCountBlock / 64; ++w) chunk += s_red[w];
+    if (running + chunk >= 0xFFFFFFFFull) {  // block-uniform decision
+      flush();
+      running = 0;
+    }
+    running += chunk;
+    if (uniform) {
+      if (am && lane == leader) {
+        atomicAdd(&s_pk[id0], (uint32_t)__popcll(am));
+        atomicAdd(&s_by[id0], (uint32_t)ws);
+      }
+    } else if (mine) {
+      atomicAdd(&s_pk[id], 1u);
+      atomicAdd(&s_by[id], len);
+    }
+    __syncthreads();  // s_red reuse
+  }
+  if (use_lds) flush();
 }
 
 __global__ void k_finalize(BatchState* b, PersistState* p, uint64_t out_cap, uint64_t* out_n,
@@ -634,9 +705,8 @@ hipError_t launch_rank(const RankArgs& r, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_gather_ids(uint32_t* ids, uint64_t cap, const BatchState* b, FlowTable t,
-                             hipStream_t s) {
-  hipLaunchKernelGGL(k_gather, dim3(2048), dim3(kBlock), 0, s, ids, cap, b, t);
+hipError_t launch_count(const CountArgs& c, unsigned grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_count, dim3(grid), dim3(kCountBlock), 0, s, c);
   return hipGetLastError();
 }
 

@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench. Each GPU step has its own
+# time limit; a crash/abort/timeout (anything but pass/fail) stops the script.
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name: $*" >&2
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" >&2
+  tail -25 "gpurun_out/$name.log" >&2
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)" >&2; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    tests)  step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    tests-all)  step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+    smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)  step bench 600 python bench.py ;;
+    bench-short) step bench 600 python bench.py --steps 10 --cpu-seconds 6 ;;
+    sweep)  step sweep 900 python tools/k1_sweep.py ;;
+    prof)   step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --no-cpu --no-extra ;;
+    *) echo "unknown step $s" >&2; exit 2 ;;
+  esac
+done
