@@ -18,6 +18,8 @@
 //   k_finalize     counters (counters.rs) + record count + running bases.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "tcbee_gen.h"
 #include "tcbee_internal.h"
 #include "tcbee_layout.h"
@@ -51,6 +53,9 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 }
 
 constexpr uint32_t kSpinLimit = 1u << 24;
+constexpr int kAuxSc1 = 16;   // buffer cache-policy bits: sc1 (agent coherence, bypass L1)
+constexpr int kAuxPlain = 0;  // plain: L1/L2 allocating
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // 16 bytes at arena[a .. a+16), zero past arena_len (a is 16-B aligned).
 __device__ __forceinline__ uint4 load_chunk(const uint8_t* arena, uint64_t arena_len, uint64_t a) {
@@ -79,16 +84,35 @@ __device__ __forceinline__ bool parse_frame(const uint8_t* __restrict__ arena, u
   else if (caplen > arena_len - off) caplen = (uint32_t)(arena_len - off);
   if (caplen < kEthHdrLen) return false;  // xdp.rs:37-39
 
-  // Load the header window: 16-B aligned chunks covering [off, off+min(len,74)).
+  // Load the header window in 16-B aligned chunks: [off, off+min(len,54)) first
+  // (all an IPv4 frame needs), the rest up to 74 B only for IPv6 frames.
   const uint64_t abase = off & ~15ull;
   const uint32_t s = (uint32_t)(off & 15u);
-  const uint32_t need = s + (caplen < 74u ? caplen : 74u);
+  const uint32_t need4 = s + (caplen < kV4MinLen ? caplen : kV4MinLen);
   uint32_t w[24];
 #pragma unroll
   for (int c = 0; c < 6; ++c) {
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if ((uint32_t)(16 * c) < need) v = load_chunk(arena, arena_len, abase + 16u * c);
+    if (c < 5 && (uint32_t)(16 * c) < need4) v = load_chunk(arena, arena_len, abase + 16u * c);
     w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+  }
+  {
+    // ethertype straight from the raw window: bytes s+12, s+13 (dwords 3..7)
+    const uint32_t e = s + 12, t3 = (e >> 2) - 3, m1 = 0u - (t3 & 1u), m2 = 0u - ((t3 >> 1) & 1u);
+    const uint32_t x0 = (w[3] & ~m1) | (w[4] & m1), x1 = (w[4] & ~m1) | (w[5] & m1);
+    const uint32_t x2 = (w[5] & ~m1) | (w[6] & m1), x3 = (w[6] & ~m1) | (w[7] & m1);
+    const uint32_t lo = (x0 & ~m2) | (x2 & m2), hi = (x1 & ~m2) | (x3 & m2);
+    const uint32_t et = bswap16(align_bytes(hi, lo, e & 3u) & 0xFFFFu);
+    const uint32_t need6 = s + (caplen < kV6MinLen ? caplen : kV6MinLen);
+    if (et == kEthertypeIPv6 && need6 > need4) {
+#pragma unroll
+      for (int c = 3; c < 6; ++c) {
+        if ((uint32_t)(16 * c) >= need4 && (uint32_t)(16 * c) < need6) {
+          const uint4 v = load_chunk(arena, arena_len, abase + 16u * c);
+          w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+        }
+      }
+    }
   }
   // Normalise so that u[j] holds frame bytes [4j, 4j+4): shift by s bytes
   // (dword shift by s>>2 via two select stages, then a byte align by s&3).
@@ -304,7 +328,7 @@ __device__ __forceinline__ void lds_put_record(uint32_t* srec, uint32_t bo, cons
 // ---------------------------------------------------------------------------
 // K1
 // ---------------------------------------------------------------------------
-template <int FPL, bool FLOWS>
+template <int FPL, bool FLOWS, int PROBE_AUX>
 __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   constexpr int TILE = kBlock * FPL;
   constexpr int SREC_DW = (TILE * kRecBytes + 32) / 4;
@@ -323,7 +347,9 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   bool acc[FPL];
   uint32_t rank[FPL], slot[FPL], hsh[FPL], clen[FPL];
   uint64_t fs_seen[FPL];
+  uint64_t K[FPL][5];
 
+  // phase A: every frame of the lane is loaded and parsed (loads in flight together)
 #pragma unroll
   for (int f = 0; f < FPL; ++f) {
     const uint64_t i = i0 + (uint64_t)f * kBlock + tid;
@@ -332,34 +358,78 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
     hsh[f] = 0;
     clen[f] = 0;
     fs_seen[f] = ~0ull;
-    uint64_t K[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 5; ++j) K[f][j] = 0;
     if (i < a.n) {
       const uint64_t off = a.offset[i];
       clen[f] = a.caplen[i];
       const uint64_t ts = a.ts[i];
-      acc[f] = parse_frame(a.arena, a.arena_len, off, clen[f], ts, a.filter_port, R[f], K);
+      acc[f] = parse_frame(a.arena, a.arena_len, off, clen[f], ts, a.filter_port, R[f], K[f]);
     }
-    if (FLOWS) {
-      const uint64_t am = __ballot(acc[f]);
-      if (am) {
-        // wave-uniform key (one flow in the whole wave): one lane probes
-        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)am) - 1;
-        bool same = true;
+  }
+  if (FLOWS) {
+    // phase B: hash, then issue the first probe's slot-line loads of every frame
+    uint64_t h[FPL], W[FPL][7];
+    const __amdgpu_buffer_rsrc_t meta_rs = __builtin_amdgcn_make_buffer_rsrc(
+        a.tab.meta, 0, (int)((a.tab.mask + 1) * 64u > 0x7FFFFFFFull ? 0x7FFFFFFF : (a.tab.mask + 1) * 64u),
+        0x00020000);
+    bool uni[FPL], want[FPL];
+    uint32_t leader[FPL];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) same = same && (!acc[f] || K[j] == __shfl(K[j], leader));
-        const uint64_t h = flow_hash64(K[0], K[1], K[2], K[3], K[4]);
-        if (acc[f]) hsh[f] = fold32(h);
-        if (__all(same)) {
-          uint32_t sl = 0xFFFFFFFFu;
-          uint64_t fs = ~0ull;
-          if (lane == leader) sl = flow_upsert(a.tab, K, h, a.batch, a.new_list, a.persist, fs);
-          slot[f] = __shfl(sl, leader);
-          fs_seen[f] = __shfl(fs, leader);
-        } else if (acc[f]) {
-          slot[f] = flow_upsert(a.tab, K, h, a.batch, a.new_list, a.persist, fs_seen[f]);
+    for (int f = 0; f < FPL; ++f) {
+      const uint64_t am = __ballot(acc[f]);
+      leader[f] = am ? (uint32_t)__ffsll((unsigned long long)am) - 1 : 0u;
+      bool same = true;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) same = same && (!acc[f] || K[f][j] == __shfl(K[f][j], leader[f]));
+      // wave-uniform key (one flow in the whole wave): only the leader probes
+      uni[f] = am != 0 && __all(same);
+      h[f] = flow_hash64(K[f][0], K[f][1], K[f][2], K[f][3], K[f][4]);
+      if (acc[f]) hsh[f] = fold32(h[f]);
+      want[f] = uni[f] ? lane == leader[f] : acc[f];
+      if (want[f]) {
+        // The 64-B slot as 4 x 16-B loads. Plain (cacheable) loads are exact here:
+        // a slot never straddles a cache line and the claimer stores the key
+        // (drained) before the tag, so any snapshot that shows this flow's tag
+        // also shows its key; a stale snapshot shows EMPTY/BUSY or a mismatch,
+        // and every such miss falls through to flow_upsert's coherent path.
+        const uint32_t off = (uint32_t)((h[f] & a.tab.mask) * 64u);
+        u32x4 q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = __builtin_amdgcn_raw_buffer_load_b128(meta_rs, off + 16u * j, 0, PROBE_AUX);
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+          const u32x4 v = q[j >> 1];
+          W[f][j] = (j & 1) ? ((uint64_t)v[2] | ((uint64_t)v[3] << 32)) : ((uint64_t)v[0] | ((uint64_t)v[1] << 32));
         }
       }
     }
+    // phase C: resolve; a miss (new flow, collision, busy slot) takes the full upsert
+#pragma unroll
+    for (int f = 0; f < FPL; ++f) {
+      uint32_t sl = 0xFFFFFFFFu;
+      uint64_t fs = ~0ull;
+      if (want[f]) {
+        const bool hit = W[f][0] == hash_tag(h[f]) && W[f][1] == K[f][0] && W[f][2] == K[f][1] &&
+                         W[f][3] == K[f][2] && W[f][4] == K[f][3] && W[f][5] == K[f][4];
+        if (hit) {
+          sl = (uint32_t)(h[f] & a.tab.mask);
+          fs = W[f][6];
+        } else {
+          sl = flow_upsert(a.tab, K[f], h[f], a.batch, a.new_list, a.persist, fs);
+        }
+      }
+      if (uni[f]) {
+        slot[f] = __shfl(sl, leader[f]);
+        fs_seen[f] = __shfl(fs, leader[f]);
+      } else if (acc[f]) {
+        slot[f] = sl;
+        fs_seen[f] = fs;
+      }
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < FPL; ++f) {
     const uint64_t b = __ballot(acc[f]);
     if (lane == 0) s_wcnt[f][wave] = (uint32_t)__popcll(b);
     rank[f] = (uint32_t)__popcll(b & lanemask_lt());
@@ -683,8 +753,18 @@ hipError_t launch_table_init(FlowTable t, hipStream_t s) {
 template <int FPL>
 static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s) {
   const dim3 grid((unsigned)a.ntiles);
-  if (flows) hipLaunchKernelGGL((k_parse<FPL, true>), grid, dim3(kBlock), 0, s, a);
-  else hipLaunchKernelGGL((k_parse<FPL, false>), grid, dim3(kBlock), 0, s, a);
+  // probe-load cache policy: plain (L1/L2-allocating) by default; TCBEE_PROBE_AUX=16
+  // selects sc1 (agent-coherent, bypasses L1) for A/B runs
+  static const int aux = [] {
+    const char* e = getenv("TCBEE_PROBE_AUX");
+    return e ? atoi(e) : kAuxPlain;
+  }();
+  if (flows) {
+    if (aux == kAuxSc1) hipLaunchKernelGGL((k_parse<FPL, true, kAuxSc1>), grid, dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain>), grid, dim3(kBlock), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain>), grid, dim3(kBlock), 0, s, a);
+  }
   return hipGetLastError();
 }
 

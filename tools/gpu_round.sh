@@ -22,6 +22,10 @@ for s in "$@"; do
     bench)  step bench 600 python bench.py ;;
     bench-short) step bench 600 python bench.py --steps 10 --cpu-seconds 6 ;;
     sweep)  step sweep 900 python tools/k1_sweep.py ;;
+    sweep2) step sweep 900 python tools/k1_sweep.py --fpl 2,4 --workloads imix10k,imix1,64B1 ;;
+    sweep1m) step sweep1m 900 python tools/k1_sweep.py --frames 1000000 --fpl 1,2,4 --workloads 64B1,imix10k --rounds 5 --iters 20 ;;
+    pmc)    step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 3 --warmup 1 --no-cpu --no-extra && \
+            step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 3 --warmup 1 --no-cpu --no-extra ;;
     prof)   step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --no-cpu --no-extra ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
