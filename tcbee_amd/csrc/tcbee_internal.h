@@ -36,8 +36,8 @@ struct PersistState {
 struct BatchState {
   uint64_t n_acc;   // accepted frames in this batch (last tile writes it)
   uint64_t n_new;   // flows first claimed in this batch
-  uint32_t ticket;  // dynamic tile ticket
   uint32_t pad0;
+  uint32_t pad2;
   uint64_t pad1;
 };
 static_assert(sizeof(BatchState) == 32, "memset size");

@@ -53,6 +53,7 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 }
 
 constexpr uint32_t kSpinLimit = 1u << 24;
+constexpr uint32_t kRecountSpins = 4096;  // ~0.1 ms of polling before recounting
 constexpr int kAuxSc1 = 16;   // buffer cache-policy bits: sc1 (agent coherence, bypass L1)
 constexpr int kAuxPlain = 0;  // plain: L1/L2 allocating
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -75,6 +76,7 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* arena, uint64_t arena
 //   (v4: caplen >= 54 && ip[9] == 6  |  v6: caplen >= 74 && ip6[6] == 6) &&
 //   (filter_port == 0 || sport == filter_port || dport == filter_port)
 // ---------------------------------------------------------------------------
+template <bool NOLOAD = false>
 __device__ __forceinline__ bool parse_frame(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                             uint64_t off, uint32_t caplen, uint64_t ts,
                                             uint32_t filter_port, uint32_t (&R)[19],
@@ -87,13 +89,21 @@ __device__ __forceinline__ bool parse_frame(const uint8_t* __restrict__ arena, u
   // Load the header window in 16-B aligned chunks: [off, off+min(len,54)) first
   // (all an IPv4 frame needs), the rest up to 74 B only for IPv6 frames.
   const uint64_t abase = off & ~15ull;
-  const uint32_t s = (uint32_t)(off & 15u);
+  const uint32_t s = NOLOAD ? 0u : (uint32_t)(off & 15u);
   const uint32_t need4 = s + (caplen < kV4MinLen ? caplen : kV4MinLen);
   uint32_t w[24];
 #pragma unroll
   for (int c = 0; c < 6; ++c) {
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (c < 5 && (uint32_t)(16 * c) < need4) v = load_chunk(arena, arena_len, abase + 16u * c);
+    if (NOLOAD) {
+      // timing ablation: a synthetic IPv4/TCP header (8192 flows) instead of the frame
+      const uint32_t fl = (uint32_t)(off >> 6) & 8191u;
+      v = make_uint4(0x01010101u * c, 0x02020202u * c + fl, 0x03030303u * c, 0x04040404u * c);
+      if (c == 0) v.w = 0x00450008u;         // ethertype 0x0800, ver/ihl 0x45
+      if (c == 1) v.y = 0x06400000u;         // ttl 64, proto 6
+    } else if (c < 5 && (uint32_t)(16 * c) < need4) {
+      v = load_chunk(arena, arena_len, abase + 16u * c);
+    }
     w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
   }
   {
@@ -275,23 +285,42 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
   return v;
 }
 
-__device__ uint64_t lookback(uint64_t* status, uint64_t tile, uint64_t count, PersistState* persist) {
+__device__ __forceinline__ void lookback_publish(uint64_t* status, uint64_t tile, uint64_t count) {
+  st_agent(status + tile, (tile == 0 ? kFlagInc : kFlagAgg) | count);
+}
+
+template <int FPL>
+__device__ uint32_t tile_accept_count(const ParseArgs& a, uint64_t tile);
+
+// Resolves this tile's exclusive prefix (one wave) and publishes its inclusive
+// prefix. Tiles are blockIdx.x: no dispatch order is assumed. A predecessor
+// whose word stays unpublished for kRecountSpins polls (not yet dispatched, or
+// slow) has its aggregate recounted from the input by this wave, so the walk
+// always terminates; results never depend on which block publishes first.
+template <int FPL>
+__device__ uint64_t lookback_resolve(const ParseArgs& a, uint64_t tile, uint64_t count) {
   const uint32_t lane = __lane_id();
-  if (tile == 0) {
-    if (lane == 0) st_agent(status, kFlagInc | count);
-    return 0;
-  }
-  if (lane == 0) st_agent(status + tile, kFlagAgg | count);
+  if (tile == 0) return 0;
+  uint64_t* status = a.tile_status;
   uint64_t excl = 0;
   int64_t base = (int64_t)tile - 1;
   for (;;) {
     const int64_t idx = base - (int64_t)lane;
     uint64_t v = idx >= 0 ? ld_agent(status + idx) : kFlagInc;
     uint32_t spins = 0;
-    while (__any((v >> 62) == 0)) {
-      if (++spins > kSpinLimit) {
-        if (lane == 0) atomicOr(&persist->status, kStSpin);
-        break;
+    for (;;) {
+      const uint64_t inv = __ballot((v >> 62) == 0);
+      if (!inv) break;
+      // only the invalid lanes nearer than the nearest inclusive prefix matter
+      const uint64_t inc = __ballot((v >> 62) == 2);
+      const uint64_t need = inc ? (inv & ((inc & (~inc + 1)) - 1)) : inv;
+      if (!need) break;
+      if (++spins > kRecountSpins) {
+        const uint32_t j = (uint32_t)__ffsll((unsigned long long)need) - 1;
+        const uint32_t cnt = tile_accept_count<FPL>(a, (uint64_t)(base - (int64_t)j));
+        if (lane == j) v = kFlagAgg | cnt;
+        spins = 0;
+        continue;
       }
       __builtin_amdgcn_s_sleep(1);
       if ((v >> 62) == 0) v = ld_agent(status + idx);
@@ -325,21 +354,42 @@ __device__ __forceinline__ void lds_put_record(uint32_t* srec, uint32_t bo, cons
   }
 }
 
+// Accepted frames of one tile, recomputed from the input by one wave (the
+// look-back's fallback when a predecessor has not published).
+template <int FPL>
+__device__ uint32_t tile_accept_count(const ParseArgs& a, uint64_t tile) {
+  constexpr int TILE = kBlock * FPL;
+  const uint32_t lane = __lane_id();
+  uint32_t cnt = 0;
+  for (int k = 0; k < TILE / 64; ++k) {
+    const uint64_t i = tile * (uint64_t)TILE + (uint64_t)k * 64 + lane;
+    bool ok = false;
+    if (i < a.n) {
+      uint32_t R[19];
+      uint64_t K[5];
+      ok = parse_frame(a.arena, a.arena_len, a.offset[i], a.caplen[i], 0, a.filter_port, R, K);
+    }
+    cnt += (uint32_t)__popcll(__ballot(ok));
+  }
+  return cnt;
+}
+
 // ---------------------------------------------------------------------------
 // K1
 // ---------------------------------------------------------------------------
-template <int FPL, bool FLOWS, int PROBE_AUX>
+// ABL: timing-only ablation bits (0 in every product launch; see tools/ablate.py)
+//   1 no look-back, 2 no record stores, 4 no header loads, 8 no index loads,
+//   16 no side outputs
+template <int FPL, bool FLOWS, int PROBE_AUX, int ABL = 0>
 __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   constexpr int TILE = kBlock * FPL;
   constexpr int SREC_DW = (TILE * kRecBytes + 32) / 4;
   __shared__ __attribute__((aligned(16))) uint32_t s_rec[SREC_DW];
   __shared__ uint32_t s_wcnt[FPL][4];
-  __shared__ uint64_t s_tile, s_excl;
+  __shared__ uint64_t s_excl;
 
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  if (tid == 0) s_tile = atomicAdd(&a.batch->ticket, 1u);
-  __syncthreads();
-  const uint64_t tile = s_tile;
+  const uint64_t tile = blockIdx.x;
   const uint64_t i0 = tile * (uint64_t)TILE;
   const uint64_t rec_base = a.persist->rec_base;
 
@@ -361,12 +411,34 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
 #pragma unroll
     for (int j = 0; j < 5; ++j) K[f][j] = 0;
     if (i < a.n) {
-      const uint64_t off = a.offset[i];
-      clen[f] = a.caplen[i];
-      const uint64_t ts = a.ts[i];
-      acc[f] = parse_frame(a.arena, a.arena_len, off, clen[f], ts, a.filter_port, R[f], K[f]);
+      const uint64_t off = (ABL & 8) ? i * 64 : a.offset[i];
+      clen[f] = (ABL & 8) ? 64u : a.caplen[i];
+      const uint64_t ts = (ABL & 8) ? i : a.ts[i];
+      acc[f] = parse_frame<(ABL & 4) != 0>(a.arena, a.arena_len, off, clen[f], ts, a.filter_port,
+                                          R[f], K[f]);
     }
   }
+#pragma unroll
+  for (int f = 0; f < FPL; ++f) {
+    const uint64_t b = __ballot(acc[f]);
+    if (lane == 0) s_wcnt[f][wave] = (uint32_t)__popcll(b);
+    rank[f] = (uint32_t)__popcll(b & lanemask_lt());
+  }
+  __syncthreads();
+  uint32_t running = 0;
+#pragma unroll
+  for (int f = 0; f < FPL; ++f) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t c = s_wcnt[f][w];
+      if ((uint32_t)w == wave) rank[f] += running;
+      running += c;
+    }
+  }
+  const uint32_t total = running;
+  // publish this tile's aggregate as early as possible (successors look back on it)
+  if (!(ABL & 1) && tid == 0) lookback_publish(a.tile_status, tile, total);
+
   if (FLOWS) {
     // phase B: hash, then issue the first probe's slot-line loads of every frame
     uint64_t h[FPL], W[FPL][7];
@@ -428,30 +500,18 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
       }
     }
   }
+  if (!(ABL & 2)) {
 #pragma unroll
-  for (int f = 0; f < FPL; ++f) {
-    const uint64_t b = __ballot(acc[f]);
-    if (lane == 0) s_wcnt[f][wave] = (uint32_t)__popcll(b);
-    rank[f] = (uint32_t)__popcll(b & lanemask_lt());
+    for (int f = 0; f < FPL; ++f)
+      if (acc[f]) lds_put_record(s_rec, rank[f] * kRecBytes, R[f]);
+  } else {
+#pragma unroll
+    for (int f = 0; f < FPL; ++f)
+      if (acc[f]) asm volatile("" ::"v"(R[f][0]), "v"(R[f][5]), "v"(R[f][13]), "v"(R[f][17]));
   }
-  __syncthreads();
-  uint32_t running = 0;
-#pragma unroll
-  for (int f = 0; f < FPL; ++f) {
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const uint32_t c = s_wcnt[f][w];
-      if ((uint32_t)w == wave) rank[f] += running;
-      running += c;
-    }
-  }
-  const uint32_t total = running;
-#pragma unroll
-  for (int f = 0; f < FPL; ++f)
-    if (acc[f]) lds_put_record(s_rec, rank[f] * kRecBytes, R[f]);
 
   if (wave == 0) {
-    const uint64_t excl = lookback(a.tile_status, tile, total, a.persist);
+    const uint64_t excl = (ABL & 1) ? tile * (uint64_t)TILE : lookback_resolve<FPL>(a, tile, total);
     if (lane == 0) s_excl = excl;
   }
   __syncthreads();
@@ -461,7 +521,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   // ---- records: LDS -> HBM, 16-B stores, partial chunks as 2-B stores ----
   const uint64_t wr_lo = excl < a.out_cap ? excl : a.out_cap;
   const uint64_t wr_hi = (excl + total) < a.out_cap ? (excl + total) : a.out_cap;
-  if (wr_hi > wr_lo) {
+  if (!(ABL & 2) && wr_hi > wr_lo) {
     const uint64_t G0 = wr_lo * kRecBytes, G1 = wr_hi * kRecBytes;
     const uint64_t A = G0 & ~15ull;
     const uint32_t head = (uint32_t)(G0 & 15u);
@@ -497,7 +557,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
 #pragma unroll
   for (int f = 0; f < FPL; ++f) {
     const uint64_t p = excl + rank[f];
-    if (acc[f]) {
+    if (acc[f] && !(ABL & 16)) {
       if (a.out_hash && p < a.out_cap) a.out_hash[p] = hsh[f];
       if (FLOWS) {
         a.acc_slot[p] = slot[f];
@@ -759,6 +819,23 @@ static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s
     const char* e = getenv("TCBEE_PROBE_AUX");
     return e ? atoi(e) : kAuxPlain;
   }();
+  static const int abl = [] {
+    const char* e = getenv("TCBEE_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
+  if (FPL == 2 && abl) {
+#define TCBEE_ABL_CASE(B)                                                                      \
+  case B:                                                                                      \
+    if (flows) hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, B>), grid, dim3(kBlock), 0, s, a); \
+    else hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain, B>), grid, dim3(kBlock), 0, s, a);     \
+    return hipGetLastError();
+    switch (abl) {
+      TCBEE_ABL_CASE(1) TCBEE_ABL_CASE(2) TCBEE_ABL_CASE(4) TCBEE_ABL_CASE(8)
+      TCBEE_ABL_CASE(16) TCBEE_ABL_CASE(3) TCBEE_ABL_CASE(31)
+      default: break;
+    }
+#undef TCBEE_ABL_CASE
+  }
   if (flows) {
     if (aux == kAuxSc1) hipLaunchKernelGGL((k_parse<FPL, true, kAuxSc1>), grid, dim3(kBlock), 0, s, a);
     else hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain>), grid, dim3(kBlock), 0, s, a);
