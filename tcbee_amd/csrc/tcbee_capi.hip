@@ -19,6 +19,7 @@ struct tcbee_ctx {
   hipStream_t stream = nullptr;
   uint64_t max_frames = 0, max_arena = 0, max_flows = 0;
   int fpl = 2;
+  uint32_t withhold_every = 0;  // TCBEE_TEST_WITHHOLD (look-back recount test hook)
 
   FlowTable tab{};
   uint64_t nslots = 0;
@@ -170,6 +171,7 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   c->max_frames = max_frames;
   c->max_arena = max_arena;
   c->max_flows = max_flows < 16 ? 16 : max_flows;
+  if (const char* e = std::getenv("TCBEE_TEST_WITHHOLD")) c->withhold_every = (uint32_t)std::atoi(e);
   if (const char* e = std::getenv("TCBEE_FPL")) {
     const int v = std::atoi(e);
     if (v == 1 || v == 2 || v == 4) c->fpl = v;
@@ -270,6 +272,7 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     a.new_list = c->d_new_list;
     a.tab = c->tab;
     a.filter_port = cfg->filter_port;
+    a.withhold_every = c->withhold_every;
     const bool timed = c->profiling && c->ev_used < kMaxProfiled;
     if (timed) TRY_HIP(hipEventRecord(c->ev[2 * c->ev_used], s));
     TRY_HIP(launch_parse(a, fpl, flows, s));

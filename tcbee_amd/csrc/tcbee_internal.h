@@ -61,6 +61,7 @@ struct ParseArgs {
   uint64_t* new_list;     // slots first claimed this batch
   FlowTable tab;
   uint16_t filter_port;
+  uint32_t withhold_every;  // test hook (TCBEE_TEST_WITHHOLD): 0 in production
 };
 
 struct RankArgs {

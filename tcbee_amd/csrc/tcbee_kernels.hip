@@ -298,7 +298,8 @@ __device__ uint32_t tile_accept_count(const ParseArgs& a, uint64_t tile);
 // slow) has its aggregate recounted from the input by this wave, so the walk
 // always terminates; results never depend on which block publishes first.
 template <int FPL>
-__device__ uint64_t lookback_resolve(const ParseArgs& a, uint64_t tile, uint64_t count) {
+__device__ uint64_t lookback_resolve(const ParseArgs& a, uint64_t tile, uint64_t count,
+                                    bool withhold) {
   const uint32_t lane = __lane_id();
   if (tile == 0) return 0;
   uint64_t* status = a.tile_status;
@@ -334,7 +335,7 @@ __device__ uint64_t lookback_resolve(const ParseArgs& a, uint64_t tile, uint64_t
     excl += wave_sum64(v & kValMask);
     base -= 64;
   }
-  if (lane == 0) st_agent(status + tile, kFlagInc | (excl + count));
+  if (lane == 0 && !withhold) st_agent(status + tile, kFlagInc | (excl + count));
   return excl;
 }
 
@@ -437,7 +438,10 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   }
   const uint32_t total = running;
   // publish this tile's aggregate as early as possible (successors look back on it)
-  if (!(ABL & 1) && tid == 0) lookback_publish(a.tile_status, tile, total);
+  // (a.withhold_every: test hook, tiles t % k == k-1 never publish, forcing their
+  //  successors down the recount path)
+  const bool withhold = a.withhold_every && (tile % a.withhold_every) == a.withhold_every - 1;
+  if (!(ABL & 1) && !withhold && tid == 0) lookback_publish(a.tile_status, tile, total);
 
   if (FLOWS) {
     // phase B: hash, then issue the first probe's slot-line loads of every frame
@@ -511,7 +515,8 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   }
 
   if (wave == 0) {
-    const uint64_t excl = (ABL & 1) ? tile * (uint64_t)TILE : lookback_resolve<FPL>(a, tile, total);
+    const uint64_t excl =
+        (ABL & 1) ? tile * (uint64_t)TILE : lookback_resolve<FPL>(a, tile, total, withhold);
     if (lane == 0) s_excl = excl;
   }
   __syncthreads();

@@ -186,6 +186,18 @@ def test_tile_shape_determinism(gpu, oracle, fpl, monkeypatch):
         assert_same(p.parse(tr), oracle.parse(tr), p.flows())
 
 
+@pytest.mark.parametrize("every", ["1", "3", "64"])
+def test_lookback_recount_fallback(gpu, oracle, every, monkeypatch):
+    """Tiles that never publish force successors to recount them from the input:
+    results stay exact (the look-back assumes no dispatch order)."""
+    from tracegen import mixed_trace
+    monkeypatch.setenv("TCBEE_TEST_WITHHOLD", every)
+    tr = mixed_trace(20_000 if every == "1" else 60_000, seed=91, n_flows=300)
+    with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 25, max_flows=1 << 12) as p:
+        assert_same(p.parse(tr), oracle.parse(tr), p.flows())
+        assert p.status() == 0
+
+
 def test_flow_table_full_reports(gpu):
     from tracegen import mixed_trace
     tr = mixed_trace(50_000, seed=5, n_flows=5000)
