@@ -6,9 +6,11 @@ Workload (config 3 of BASELINE.json, the largest single-GPU config): per GPU,
 10k flows, all resident in HBM before the timed region. A step = one
 ``tcbee_parse_batch_device`` over the whole batch: parse + 74-B records +
 flow hash + flow classification (table upsert, dense first-seen ids) +
-counters. With --gpus N each rank parses its own contiguous shard of one global
-trace (weak scaling, no data-path collective); the per-rank counters are summed
-over RCCL once per step.
+counters. Each step is one fresh trace (the flow table starts empty). With
+--gpus N each rank parses its own contiguous shard of one global trace (weak
+scaling, no frame exchange); per step the compact per-rank flow tables are
+all-gathered over RCCL, merged on every GPU (global dense first-seen ids) and
+each rank's record flow ids are remapped; the counters are all-reduced.
 
 Prints ONE JSON line (rank 0). See DESIGN.md "Measurement".
 """
@@ -62,13 +64,24 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     d_id = torch.empty(n, dtype=torch.int32, device="cuda")
     d_n = torch.zeros(1, dtype=torch.int64, device="cuda")
     d_ctr = torch.zeros(4, dtype=torch.int64, device="cuda")
+    cap = max(4 * n_flows, 1 << 12)
     p = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=n, max_arena=0,
-                               max_flows=max(4 * n_flows, 1 << 12))
+                               max_flows=cap)
+    merged = fm = None
+    if world > 1:
+        from tcbee_amd.dist import FlowMerge
+        merged = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=1024,
+                                        max_arena=0, max_flows=world * cap)
+        fm = FlowMerge(p, merged, cap, world * n)
 
     def step():
+        # one step = one fresh trace: empty flow table, parse + classify the shard,
+        # then (N>1) the RCCL flow-table merge and the local->global id remap
+        p.reset_flows(stream=stream, sync=False)
         p.parse_device(d_arena, alen, d_off, d_len, d_ts, n, d_rec, n, d_hash, d_id, d_n,
                        d_ctr, stream=stream)
         if world > 1:
+            fm.step(d_id, d_n, n, stream=stream)
             dist.all_reduce(d_ctr)  # RCCL: global INGRESS/HANDLED/DROPPED
 
     for _ in range(warmup):
@@ -91,12 +104,15 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
 
     # validation (untimed): counts, flow table, and a bit-exact sample vs the oracle
     nrec = int(d_n.item())
-    flows = p.flows()
-    check = {"records": nrec, "flows": int(len(flows)), "status": status}
+    flows = (merged if merged is not None else p).flows()
+    check = {"records": nrec, "flows": int(len(flows)), "status": status,
+             "pkts_total": int(flows["pkts"].sum())}
     if rank == 0:
         check.update(validate_sample(torch, d_rec, d_hash, n, sizes, kind, n_flows, seed,
                                      first, nrec))
     p.close()
+    if merged is not None:
+        merged.close()
     del d_arena, d_rec
     torch.cuda.empty_cache()
     return elapsed, k1_ms / max(k1_launches, 1), nrec, check

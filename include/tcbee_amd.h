@@ -168,6 +168,30 @@ int tcbee_flow_export(tcbee_ctx* ctx, tcbee_flow_entry* out_host, uint64_t cap,
                       uint64_t* n);
 /* Forget every flow (ids restart at 0, record index restarts at 0). */
 int tcbee_flow_reset(tcbee_ctx* ctx);
+/* Device-side export: out_dev[id] for every flow id < cap (async on stream);
+ * n_dev (device u64[2], may be NULL) receives {min(flow count, cap), accepted
+ * frames so far} — exactly one segment's entry of seg_meta below. */
+int tcbee_flow_export_device(tcbee_ctx* ctx, tcbee_flow_entry* out_dev, uint64_t cap,
+                             uint64_t* n_dev, void* stream);
+/* Multi-GPU merge. ent_dev holds nseg segments of `stride`
+ * entries: segment r = rank r's exported table; seg_meta_dev[2r] = its valid
+ * entries, seg_meta_dev[2r+1] = its records (segments are consecutive slices of
+ * one global record stream, first_seen local to the segment). The context's
+ * table is REPLACED by the merge: flows equal by key are one flow, pkts/bytes
+ * summed, first_seen = (records of earlier segments) + local first_seen,
+ * minimised, dense ids in global first-seen order. out_ids_dev[r*stride + j] =
+ * merged id of entry j of segment r (rank r's local-to-global id map).
+ * max_total_records bounds the global record count. Asynchronous; the first
+ * merge (or a larger bound) allocates scratch and synchronizes. */
+int tcbee_flow_merge_device(tcbee_ctx* ctx, const tcbee_flow_entry* ent_dev,
+                            uint64_t nseg, uint64_t stride, const uint64_t* seg_meta_dev,
+                            uint64_t max_total_records, uint32_t* out_ids_dev, void* stream);
+/* ids[p] = map[ids[p]] for p < min(*n_dev, n_max) (n_dev may be NULL);
+ * ids >= map_len or 0xFFFFFFFF become 0xFFFFFFFF: local ids -> merged ids. */
+int tcbee_remap_ids_device(uint32_t* ids_dev, uint64_t n_max, const uint64_t* n_dev,
+                           const uint32_t* map_dev, uint64_t map_len, void* stream);
+/* The same, asynchronous on `stream` (NULL = the context's stream). */
+int tcbee_flow_reset_device(tcbee_ctx* ctx, void* stream);
 /* Sticky status of the last batches: TCBEE_OK, TCBEE_EFLOWFULL or TCBEE_ESPIN.
  * Synchronous; clears the status. */
 int tcbee_ctx_status(tcbee_ctx* ctx);

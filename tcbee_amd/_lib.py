@@ -86,7 +86,14 @@ _SIGS = {
     "tcbee_flow_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64,
                                     C.POINTER(C.c_uint64)]),
     "tcbee_flow_reset": (C.c_int, [C.c_void_p]),
+    "tcbee_flow_reset_device": (C.c_int, [C.c_void_p, C.c_void_p]),
     "tcbee_ctx_status": (C.c_int, [C.c_void_p]),
+    "tcbee_flow_export_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                           C.c_void_p]),
+    "tcbee_flow_merge_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
+                                          C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "tcbee_remap_ids_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                         C.c_uint64, C.c_void_p]),
     "tcbee_ctx_profile": (C.c_int, [C.c_void_p, C.c_int]),
     "tcbee_ctx_profile_read": (C.c_int, [C.c_void_p, C.POINTER(C.c_double),
                                          C.POINTER(C.c_uint64)]),

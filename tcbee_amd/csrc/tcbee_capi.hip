@@ -47,6 +47,13 @@ struct tcbee_ctx {
   uint64_t* d_n = nullptr;
   tcbee_counters* d_ctr = nullptr;
 
+  // multi-table merge scratch (allocated on first merge, grown on demand)
+  uint64_t* d_mcnt = nullptr;
+  uint32_t* d_mbitmap = nullptr;
+  uint32_t* d_mwprefix = nullptr;
+  uint32_t* d_mbprefix = nullptr;
+  uint64_t m_words = 0;
+
   // K1 timing (tcbee_ctx_profile)
   bool profiling = false;
   std::vector<hipEvent_t> ev;  // pairs
@@ -152,6 +159,10 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
   dfree(c->d_id);
   dfree(c->d_n);
   dfree(c->d_ctr);
+  dfree(c->d_mcnt);
+  dfree(c->d_mbitmap);
+  dfree(c->d_mwprefix);
+  dfree(c->d_mbprefix);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -230,6 +241,15 @@ int tcbee_flow_reset(tcbee_ctx* c) {
   TRY_HIP(launch_table_init(c->tab, c->stream));
   TRY_HIP(hipMemsetAsync(c->d_persist, 0, sizeof(PersistState), c->stream));
   TRY_HIP(hipStreamSynchronize(c->stream));
+  return TCBEE_OK;
+}
+
+int tcbee_flow_reset_device(tcbee_ctx* c, void* stream) {
+  if (!c) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  TRY_HIP(launch_table_init(c->tab, s));
+  TRY_HIP(hipMemsetAsync(c->d_persist, 0, sizeof(PersistState), s));
   return TCBEE_OK;
 }
 
@@ -399,6 +419,78 @@ int tcbee_flow_export(tcbee_ctx* c, tcbee_flow_entry* out, uint64_t cap, uint64_
   }
   *n = p.flow_count < cap ? p.flow_count : cap;
   (void)written;
+  return TCBEE_OK;
+}
+
+int tcbee_flow_export_device(tcbee_ctx* c, tcbee_flow_entry* out_dev, uint64_t cap,
+                             uint64_t* n_dev, void* stream) {
+  if (!c || (cap && !out_dev)) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  TRY_HIP(launch_export(c->tab, reinterpret_cast<uint64_t*>(out_dev), cap, c->d_persist, n_dev, s));
+  return TCBEE_OK;
+}
+
+int tcbee_flow_merge_device(tcbee_ctx* c, const tcbee_flow_entry* ent_dev, uint64_t nseg,
+                            uint64_t stride, const uint64_t* seg_meta_dev,
+                            uint64_t max_total_records, uint32_t* out_ids_dev, void* stream) {
+  if (!c || !seg_meta_dev || (nseg * stride && (!ent_dev || !out_ids_dev))) return TCBEE_EINVAL;
+  const uint64_t total_records = max_total_records;
+  TRY_HIP(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  const uint64_t words = (total_records + 31) / 32 + 1;
+  if (!c->d_mcnt) TRY_HIP(dalloc(&c->d_mcnt, 2 * c->nslots));
+  if (words > c->m_words) {
+    // merge scratch grows with the global record count (not on the hot path)
+    TRY_HIP(hipStreamSynchronize(s));
+    dfree(c->d_mbitmap);
+    dfree(c->d_mwprefix);
+    dfree(c->d_mbprefix);
+    c->d_mbitmap = nullptr;
+    c->d_mwprefix = nullptr;
+    c->d_mbprefix = nullptr;
+    c->m_words = 0;
+    TRY_HIP(dalloc(&c->d_mbitmap, words));
+    TRY_HIP(dalloc(&c->d_mwprefix, words));
+    TRY_HIP(dalloc(&c->d_mbprefix, (words + kScanWordsPerBlock - 1) / kScanWordsPerBlock));
+    c->m_words = words;
+  }
+  // fresh table: the merge result replaces whatever this context held
+  TRY_HIP(launch_table_init(c->tab, s));
+  TRY_HIP(hipMemsetAsync(c->d_persist, 0, sizeof(PersistState), s));
+  TRY_HIP(hipMemsetAsync(c->d_batch, 0, sizeof(BatchState), s));
+  TRY_HIP(hipMemsetAsync(c->d_mcnt, 0, 2 * c->nslots * sizeof(uint64_t), s));
+  TRY_HIP(hipMemsetAsync(c->d_mbitmap, 0, words * sizeof(uint32_t), s));
+  MergeArgs g{};
+  g.ent = reinterpret_cast<const uint64_t*>(ent_dev);
+  g.nseg = nseg;
+  g.stride = stride;
+  g.seg_meta = seg_meta_dev;
+  g.tab = c->tab;
+  g.batch = c->d_batch;
+  g.persist = c->d_persist;
+  g.new_list = c->d_new_list;
+  g.mcnt = c->d_mcnt;
+  g.out_slot = out_ids_dev;
+  RankArgs r{};
+  r.new_list = c->d_new_list;
+  r.batch = c->d_batch;
+  r.persist = c->d_persist;
+  r.tab = c->tab;
+  r.bitmap = c->d_mbitmap;
+  r.wprefix = c->d_mwprefix;
+  r.bprefix = c->d_mbprefix;
+  r.nwords = words;
+  r.nblocks = (words + kScanWordsPerBlock - 1) / kScanWordsPerBlock;
+  TRY_HIP(launch_merge(g, r, s));
+  return TCBEE_OK;
+}
+
+int tcbee_remap_ids_device(uint32_t* ids_dev, uint64_t n_max, const uint64_t* n_dev,
+                           const uint32_t* map_dev, uint64_t map_len, void* stream) {
+  if (n_max && (!ids_dev || !map_dev)) return TCBEE_EINVAL;
+  if (!n_max) return TCBEE_OK;
+  TRY_HIP(launch_remap(ids_dev, n_max, n_dev, map_dev, map_len, (hipStream_t)stream));
   return TCBEE_OK;
 }
 

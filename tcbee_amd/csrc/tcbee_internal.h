@@ -91,6 +91,23 @@ struct CountArgs {
   uint64_t* cnt;
 };
 hipError_t launch_count(const CountArgs& c, unsigned grid, hipStream_t s);
+
+struct MergeArgs {
+  const uint64_t* ent;        // nseg * stride entries, tcbee_flow_entry as u64[8]
+  uint64_t nseg, stride;
+  const uint64_t* seg_meta;   // per segment {valid entries, records}
+  FlowTable tab;
+  BatchState* batch;
+  PersistState* persist;
+  uint64_t* new_list;
+  uint64_t* mcnt;             // per-slot pkts/bytes (2 * slots), zeroed
+  uint32_t* out_slot;         // per entry: slot, then merged id
+};
+hipError_t launch_export(FlowTable t, uint64_t* out, uint64_t cap, const PersistState* p,
+                         uint64_t* n_out, hipStream_t s);
+hipError_t launch_merge(const MergeArgs& g, const RankArgs& r, hipStream_t s);
+hipError_t launch_remap(uint32_t* ids, uint64_t n_max, const uint64_t* n_dev, const uint32_t* map,
+                        uint64_t map_len, hipStream_t s);
 hipError_t launch_finalize(BatchState* b, PersistState* p, uint64_t out_cap,
                            uint64_t* out_n, tcbee_counters* ctr, int direction,
                            hipStream_t s);

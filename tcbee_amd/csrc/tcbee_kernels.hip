@@ -614,7 +614,7 @@ __global__ void k_mark(RankArgs r) {
        j += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t s = r.new_list[j];
     const uint64_t local = r.tab.meta[8 * s + 6] - base;
-    atomicOr(&r.bitmap[local >> 5], 1u << (local & 31));
+    if ((local >> 5) < r.nwords) atomicOr(&r.bitmap[local >> 5], 1u << (local & 31));
   }
 }
 
@@ -788,6 +788,94 @@ __global__ void k_finalize(BatchState* b, PersistState* p, uint64_t out_cap, uin
 }
 
 // ---------------------------------------------------------------------------
+// flow-table export / multi-table merge / id remap (multi-GPU row of DESIGN.md §7)
+// An entry is tcbee_flow_entry viewed as u64[8]: key k0..k4, pkts, bytes, first_seen.
+// ---------------------------------------------------------------------------
+__global__ void k_export(FlowTable t, uint64_t* out, uint64_t cap, const PersistState* p,
+                         uint64_t* n_out) {
+  const uint64_t nslots = t.mask + 1;
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < nslots;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t* m = t.meta + 8 * s;
+    if (m[0] < 2 || m[7] == 0) continue;
+    const uint64_t id = m[7] - 1;
+    if (id >= cap) continue;
+    uint64_t* e = out + 8 * id;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) e[j] = m[1 + j];
+    e[5] = t.cnt[2 * id];
+    e[6] = t.cnt[2 * id + 1];
+    e[7] = m[6];
+  }
+  if (n_out && blockIdx.x == 0 && threadIdx.x == 0) {
+    n_out[0] = p->flow_count < cap ? p->flow_count : cap;
+    n_out[1] = p->rec_base;  // accepted frames so far = records of this segment
+  }
+}
+
+// Inserts every valid entry of nseg segments (segment r = rank r's local table,
+// first_seen local to that rank) with first_seen rebased to the global record
+// index; per-slot counters summed. out_slot[e] = merged slot (or ~0).
+__global__ void k_merge_insert(MergeArgs g) {
+  const uint64_t total = g.nseg * g.stride;
+  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
+       e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t seg = e / g.stride, j = e % g.stride;
+    if (j >= g.seg_meta[2 * seg]) {
+      g.out_slot[e] = 0xFFFFFFFFu;
+      continue;
+    }
+    const uint64_t* E = g.ent + 8 * e;
+    const uint64_t K[5] = {E[0], E[1], E[2], E[3], E[4]};
+    uint64_t fs = ~0ull;
+    const uint32_t s = flow_upsert(g.tab, K, flow_hash64(K[0], K[1], K[2], K[3], K[4]), g.batch,
+                                   g.new_list, g.persist, fs);
+    g.out_slot[e] = s;
+    if (s == 0xFFFFFFFFu) continue;
+    atomicAdd((unsigned long long*)&g.mcnt[2ull * s], (unsigned long long)E[5]);
+    atomicAdd((unsigned long long*)&g.mcnt[2ull * s + 1], (unsigned long long)E[6]);
+    uint64_t base = 0;  // records of the segments before this one
+    for (uint64_t q = 0; q < seg; ++q) base += g.seg_meta[2 * q + 1];
+    atomicMin((unsigned long long*)&g.tab.meta[8ull * s + 6], (unsigned long long)(base + E[7]));
+  }
+}
+
+// entry slot -> merged dense id; per-slot counters -> by-id counters; flow count
+__global__ void k_merge_finish(MergeArgs g) {
+  const uint64_t total = g.nseg * g.stride;
+  const uint64_t nslots = g.tab.mask + 1;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  for (uint64_t e = t0; e < total; e += stride) {
+    const uint32_t s = g.out_slot[e];
+    g.out_slot[e] = s == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(g.tab.meta[8ull * s + 7] - 1);
+  }
+  for (uint64_t s = t0; s < nslots; s += stride) {
+    const uint64_t* m = g.tab.meta + 8 * s;
+    if (m[0] < 2 || m[7] == 0) continue;
+    const uint64_t id = m[7] - 1;
+    g.tab.cnt[2 * id] = g.mcnt[2 * s];
+    g.tab.cnt[2 * id + 1] = g.mcnt[2 * s + 1];
+  }
+  if (t0 == 0) {
+    uint64_t recs = 0;
+    for (uint64_t q = 0; q < g.nseg; ++q) recs += g.seg_meta[2 * q + 1];
+    g.persist->flow_count += g.batch->n_new;
+    g.persist->rec_base += recs;
+  }
+}
+
+__global__ void k_remap(uint32_t* ids, uint64_t n_max, const uint64_t* n_dev, const uint32_t* map,
+                        uint64_t map_len) {
+  const uint64_t n = n_dev && *n_dev < n_max ? *n_dev : n_max;
+  for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < n;
+       p += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = ids[p];
+    ids[p] = v < map_len ? map[v] : 0xFFFFFFFFu;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // synthetic trace headers (payload stays as the caller zeroed it)
 // ---------------------------------------------------------------------------
 __global__ void k_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
@@ -875,6 +963,29 @@ hipError_t launch_count(const CountArgs& c, unsigned grid, hipStream_t s) {
 hipError_t launch_finalize(BatchState* b, PersistState* p, uint64_t out_cap, uint64_t* out_n,
                            tcbee_counters* ctr, int direction, hipStream_t s) {
   hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1), 0, s, b, p, out_cap, out_n, ctr, direction);
+  return hipGetLastError();
+}
+
+hipError_t launch_export(FlowTable t, uint64_t* out, uint64_t cap, const PersistState* p,
+                         uint64_t* n_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_export, dim3(grid_for(t.mask + 1)), dim3(kBlock), 0, s, t, out, cap, p, n_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge(const MergeArgs& g, const RankArgs& r, hipStream_t s) {
+  const unsigned grid = grid_for(g.nseg * g.stride);
+  hipLaunchKernelGGL(k_merge_insert, dim3(grid), dim3(kBlock), 0, s, g);
+  hipError_t e = launch_rank(r, s);
+  if (e != hipSuccess) return e;
+  const uint64_t work = g.nseg * g.stride > g.tab.mask + 1 ? g.nseg * g.stride : g.tab.mask + 1;
+  hipLaunchKernelGGL(k_merge_finish, dim3(grid_for(work)), dim3(kBlock), 0, s, g);
+  return hipGetLastError();
+}
+
+hipError_t launch_remap(uint32_t* ids, uint64_t n_max, const uint64_t* n_dev, const uint32_t* map,
+                        uint64_t map_len, hipStream_t s) {
+  hipLaunchKernelGGL(k_remap, dim3(grid_for(n_max)), dim3(kBlock), 0, s, ids, n_max, n_dev, map,
+                     map_len);
   return hipGetLastError();
 }
 

@@ -160,8 +160,28 @@ class PacketParser:
                                                 C.byref(n)), "tcbee_flow_export")
         return out[:n.value]
 
-    def reset_flows(self) -> None:
-        _lib.check(_lib.lib().tcbee_flow_reset(self._h), "tcbee_flow_reset")
+    def reset_flows(self, stream: int | None = None, sync: bool = True) -> None:
+        if sync:
+            _lib.check(_lib.lib().tcbee_flow_reset(self._h), "tcbee_flow_reset")
+        else:
+            _lib.check(_lib.lib().tcbee_flow_reset_device(self._h, C.c_void_p(stream or 0)),
+                       "tcbee_flow_reset_device")
+
+    # -- device-side flow tables (multi-GPU merge) ---------------
+    def export_device(self, out, cap: int, meta=None, stream: int | None = None) -> None:
+        """out[id] = flow entry (u64[8]) for ids < cap; meta (device u64[2]) receives
+        {flows exported, accepted frames so far}. Asynchronous."""
+        _lib.check(_lib.lib().tcbee_flow_export_device(
+            self._h, _ptr(out), C.c_uint64(cap), _ptr(meta), C.c_void_p(stream or 0)),
+            "tcbee_flow_export_device")
+
+    def merge_device(self, entries, nseg: int, stride: int, seg_meta, max_total_records: int,
+                     out_ids, stream: int | None = None) -> None:
+        """Replace this context's table by the merge of nseg exported tables."""
+        _lib.check(_lib.lib().tcbee_flow_merge_device(
+            self._h, _ptr(entries), C.c_uint64(nseg), C.c_uint64(stride), _ptr(seg_meta),
+            C.c_uint64(max_total_records), _ptr(out_ids), C.c_void_p(stream or 0)),
+            "tcbee_flow_merge_device")
 
 
 def gen_frames_device(arena, offset, caplen, n: int, kind: int, n_flows: int, seed: int,
@@ -171,6 +191,14 @@ def gen_frames_device(arena, offset, caplen, n: int, kind: int, n_flows: int, se
         _ptr(arena), _ptr(offset), _ptr(caplen), C.c_uint64(n), C.c_uint64(first_index), kind,
         C.c_uint64(n_flows), C.c_uint64(seed), C.c_void_p(stream or 0)),
         "tcbee_gen_frames_device")
+
+
+def remap_ids_device(ids, n_max: int, n_dev, id_map, map_len: int,
+                     stream: int | None = None) -> None:
+    """ids[p] = id_map[ids[p]] for p < min(*n_dev, n_max)."""
+    _lib.check(_lib.lib().tcbee_remap_ids_device(
+        _ptr(ids), C.c_uint64(n_max), _ptr(n_dev), _ptr(id_map), C.c_uint64(map_len),
+        C.c_void_p(stream or 0)), "tcbee_remap_ids_device")
 
 
 def flow_hash64(key40: bytes) -> int:

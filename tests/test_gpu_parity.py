@@ -198,6 +198,45 @@ def test_lookback_recount_fallback(gpu, oracle, every, monkeypatch):
         assert p.status() == 0
 
 
+@pytest.mark.parametrize("cuts", [[0, 30_000], [0, 9_000, 9_001, 21_000, 30_000],
+                                  [0, 3_000, 6_000, 9_000, 12_000, 15_000, 18_000, 21_000, 30_000]])
+def test_device_merge_matches_unsharded(gpu, oracle, cuts):
+    """Per-shard contexts -> device export -> concatenation (what the RCCL all-gather
+    delivers) -> tcbee_flow_merge_device -> remap == the oracle on the whole trace."""
+    import torch
+    from tracegen import mixed_trace
+    tr = mixed_trace(30_000, seed=12, n_flows=900)
+    full = oracle.parse(tr)
+    cap, world = 2048, len(cuts) - 1
+    ents, metas, ids = [], [], []
+    for lo, hi in zip(cuts, cuts[1:]):
+        with tcbee_amd.PacketParser(max_frames=1 << 16, max_arena=1 << 24, max_flows=1024) as p:
+            res = p.parse(tr.slice(lo, hi))
+            ent = torch.zeros((cap, 8), dtype=torch.int64, device="cuda")
+            meta = torch.zeros(2, dtype=torch.int64, device="cuda")
+            p.export_device(ent, cap, meta)
+            p.sync()
+            ents.append(ent)
+            metas.append(meta)
+            ids.append(res.flow_id)
+    with tcbee_amd.PacketParser(max_frames=1 << 10, max_flows=1 << 12) as m:
+        out_ids = torch.empty(world * cap, dtype=torch.int32, device="cuda")
+        m.merge_device(torch.cat(ents), world, cap, torch.cat(metas), tr.n, out_ids)
+        m.sync()
+        assert np.array_equal(m.flows(), full[4])
+        gids = []
+        for r, x in enumerate(ids):
+            d = torch.from_numpy(x.view(np.int32).copy()).cuda()
+            tcbee_amd.parser.remap_ids_device(d, len(x), None, out_ids[r * cap:(r + 1) * cap], cap)
+            torch.cuda.synchronize()
+            gids.append(d.cpu().numpy().view(np.uint32))
+        assert np.array_equal(np.concatenate(gids), full[2])
+        # merging again replaces the table (idempotent)
+        m.merge_device(torch.cat(ents), world, cap, torch.cat(metas), tr.n, out_ids)
+        m.sync()
+        assert np.array_equal(m.flows(), full[4])
+
+
 def test_flow_table_full_reports(gpu):
     from tracegen import mixed_trace
     tr = mixed_trace(50_000, seed=5, n_flows=5000)
