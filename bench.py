@@ -195,8 +195,15 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one process per GPU; TCBEE_DIST_BACKEND=gloo + fewer GPUs than ranks only for
+        # rehearsing the N>1 path on a 1-GPU box (ranks then share a device)
+        backend = os.environ.get("TCBEE_DIST_BACKEND", "nccl")
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     kind = 1 if args.flows > 1 else 0
