@@ -69,44 +69,84 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* arena, uint64_t arena
 }
 
 // ---------------------------------------------------------------------------
-// The per-frame hook. Returns accept; fills the record as 19 dwords (bytes
-// 0..75, of which 74 are the record; dword 18 = 0x0000FFFF) and the 40-B key.
+// The per-frame hook, split into window loads (so every load of a lane's frames
+// is in flight before the first use) and the parse proper.
 // Accept set (identical for xdp_hook and tc_hook):
 //   caplen >= 14 && ethertype in {0x0800, 0x86DD} &&
 //   (v4: caplen >= 54 && ip[9] == 6  |  v6: caplen >= 74 && ip6[6] == 6) &&
 //   (filter_port == 0 || sport == filter_port || dport == filter_port)
 // ---------------------------------------------------------------------------
-template <bool NOLOAD = false>
-__device__ __forceinline__ bool parse_frame(const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                            uint64_t off, uint32_t caplen, uint64_t ts,
-                                            uint32_t filter_port, uint32_t (&R)[19],
-                                            uint64_t (&K)[5]) {
-  // clamp to the arena: a frame never extends past arena_len
-  if (off >= arena_len) caplen = 0;
-  else if (caplen > arena_len - off) caplen = (uint32_t)(arena_len - off);
-  if (caplen < kEthHdrLen) return false;  // xdp.rs:37-39
+// a frame never extends past arena_len
+__device__ __forceinline__ uint32_t clamp_caplen(uint64_t off, uint32_t caplen, uint64_t arena_len) {
+  if (off >= arena_len) return 0;
+  return caplen > arena_len - off ? (uint32_t)(arena_len - off) : caplen;
+}
 
-  // Load the header window in 16-B aligned chunks: [off, off+min(len,54)) first
-  // (all an IPv4 frame needs), the rest up to 74 B only for IPv6 frames.
+__device__ __forceinline__ void put_chunk(uint32_t (&w)[24], int c, uint4 v) {
+  w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+}
+
+// Header window of FPL frames: 16-B aligned chunks 0..4 from off & ~15 (all an
+// IPv4 frame needs: s + 54 <= 69 < 80). When every lane's 80 B lie inside the
+// arena (the common case) all FPL x 5 loads are issued unconditionally, back to
+// back; otherwise each lane loads only the chunks of [off, off+min(len,54)),
+// bounds-checked. Chunk 5 (IPv6 tail) is loaded later, for IPv6 frames only.
+template <int FPL, bool NOLOAD>
+__device__ __forceinline__ void load_windows(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                             const uint64_t (&off)[FPL], const uint32_t (&len)[FPL],
+                                             uint32_t (&w)[FPL][24]) {
+  if (NOLOAD) {
+#pragma unroll
+    for (int f = 0; f < FPL; ++f) {
+      // timing ablation: a synthetic IPv4/TCP header (8192 flows) instead of the frame
+      const uint32_t fl = (uint32_t)(off[f] >> 6) & 8191u;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        uint4 v = make_uint4(0x01010101u * c, 0x02020202u * c + fl, 0x03030303u * c, 0x04040404u * c);
+        if (c == 0) v.w = 0x00450008u;  // ethertype 0x0800, ver/ihl 0x45
+        if (c == 1) v.y = 0x06400000u;  // ttl 64, proto 6
+        put_chunk(w[f], c, v);
+      }
+    }
+    return;
+  }
+  bool inb = true;
+#pragma unroll
+  for (int f = 0; f < FPL; ++f) inb = inb && (off[f] & ~15ull) + 80 <= arena_len;
+#pragma unroll
+  for (int f = 0; f < FPL; ++f) put_chunk(w[f], 5, make_uint4(0u, 0u, 0u, 0u));
+  if (__all(inb)) {
+#pragma unroll
+    for (int f = 0; f < FPL; ++f) {
+      const uint4* src = reinterpret_cast<const uint4*>(arena + (off[f] & ~15ull));
+#pragma unroll
+      for (int c = 0; c < 5; ++c) put_chunk(w[f], c, src[c]);
+    }
+  } else {
+#pragma unroll
+    for (int f = 0; f < FPL; ++f) {
+      const uint64_t abase = off[f] & ~15ull;
+      const uint32_t need4 = (uint32_t)(off[f] & 15u) + (len[f] < kV4MinLen ? len[f] : kV4MinLen);
+#pragma unroll
+      for (int c = 0; c < 5; ++c) {
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if ((uint32_t)(16 * c) < need4) v = load_chunk(arena, arena_len, abase + 16u * c);
+        put_chunk(w[f], c, v);
+      }
+    }
+  }
+}
+
+template <bool NOLOAD = false>
+__device__ __forceinline__ bool parse_window(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                             uint64_t off, uint32_t caplen, uint64_t ts,
+                                             uint32_t filter_port, uint32_t (&w)[24],
+                                             uint32_t (&R)[19], uint64_t (&K)[5]) {
+  if (caplen < kEthHdrLen) return false;  // xdp.rs:37-39
   const uint64_t abase = off & ~15ull;
   const uint32_t s = NOLOAD ? 0u : (uint32_t)(off & 15u);
   const uint32_t need4 = s + (caplen < kV4MinLen ? caplen : kV4MinLen);
-  uint32_t w[24];
-#pragma unroll
-  for (int c = 0; c < 6; ++c) {
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (NOLOAD) {
-      // timing ablation: a synthetic IPv4/TCP header (8192 flows) instead of the frame
-      const uint32_t fl = (uint32_t)(off >> 6) & 8191u;
-      v = make_uint4(0x01010101u * c, 0x02020202u * c + fl, 0x03030303u * c, 0x04040404u * c);
-      if (c == 0) v.w = 0x00450008u;         // ethertype 0x0800, ver/ihl 0x45
-      if (c == 1) v.y = 0x06400000u;         // ttl 64, proto 6
-    } else if (c < 5 && (uint32_t)(16 * c) < need4) {
-      v = load_chunk(arena, arena_len, abase + 16u * c);
-    }
-    w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
-  }
-  {
+  if (!NOLOAD) {
     // ethertype straight from the raw window: bytes s+12, s+13 (dwords 3..7)
     const uint32_t e = s + 12, t3 = (e >> 2) - 3, m1 = 0u - (t3 & 1u), m2 = 0u - ((t3 >> 1) & 1u);
     const uint32_t x0 = (w[3] & ~m1) | (w[4] & m1), x1 = (w[4] & ~m1) | (w[5] & m1);
@@ -115,12 +155,12 @@ __device__ __forceinline__ bool parse_frame(const uint8_t* __restrict__ arena, u
     const uint32_t et = bswap16(align_bytes(hi, lo, e & 3u) & 0xFFFFu);
     const uint32_t need6 = s + (caplen < kV6MinLen ? caplen : kV6MinLen);
     if (et == kEthertypeIPv6 && need6 > need4) {
+      // IPv6 tail: chunks of [need4, need6) not loaded yet (chunk 5, or 3..5 on
+      // the bounds-checked path, where chunks past need4 were left zero)
 #pragma unroll
       for (int c = 3; c < 6; ++c) {
-        if ((uint32_t)(16 * c) >= need4 && (uint32_t)(16 * c) < need6) {
-          const uint4 v = load_chunk(arena, arena_len, abase + 16u * c);
-          w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
-        }
+        if ((uint32_t)(16 * c) < need6 && ((uint32_t)(16 * c) >= need4 || c == 5))
+          put_chunk(w, c, load_chunk(arena, arena_len, abase + 16u * c));
       }
     }
   }
@@ -355,6 +395,17 @@ __device__ __forceinline__ void lds_put_record(uint32_t* srec, uint32_t bo, cons
   }
 }
 
+__device__ __forceinline__ bool parse_frame(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                            uint64_t off, uint32_t caplen, uint64_t ts,
+                                            uint32_t filter_port, uint32_t (&R)[19],
+                                            uint64_t (&K)[5]) {
+  const uint64_t o[1] = {off};
+  const uint32_t l[1] = {clamp_caplen(off, caplen, arena_len)};
+  uint32_t w[1][24];
+  load_windows<1, false>(arena, arena_len, o, l, w);
+  return parse_window(arena, arena_len, off, l[0], ts, filter_port, w[0], R, K);
+}
+
 // Accepted frames of one tile, recomputed from the input by one wave (the
 // look-back's fallback when a predecessor has not published).
 template <int FPL>
@@ -375,16 +426,58 @@ __device__ uint32_t tile_accept_count(const ParseArgs& a, uint64_t tile) {
   return cnt;
 }
 
+// Copies staged records [G0, G1) (global byte range; sbuf byte 0 = global byte G0)
+// to out: 16-B stores for whole chunks, 2-B stores for the partial chunks at the
+// ends (bytes there belong to neighbouring groups). Threads t0, t0+step, ...
+__device__ __forceinline__ void copy_out(uint8_t* __restrict__ out, uint64_t G0, uint64_t G1,
+                                         const uint32_t* sbuf, uint32_t t0, uint32_t step) {
+  const uint64_t A = G0 & ~15ull;
+  const uint32_t head = (uint32_t)(G0 & 15u);
+  const uint32_t nchunks = (uint32_t)((G1 - A + 15) >> 4);
+  const uint16_t* s16 = reinterpret_cast<const uint16_t*>(sbuf);
+  for (uint32_t c = t0; c < nchunks; c += step) {
+    const uint64_t g = A + 16ull * c;
+    if (g >= G0 && g + 16 <= G1) {
+      const uint32_t sb = 16u * c - head;
+      const uint32_t d0 = sb >> 2;
+      uint4 o;
+      if ((sb & 3u) == 0) {
+        o = make_uint4(sbuf[d0], sbuf[d0 + 1], sbuf[d0 + 2], sbuf[d0 + 3]);
+      } else {
+        const uint32_t x0 = sbuf[d0], x1 = sbuf[d0 + 1], x2 = sbuf[d0 + 2], x3 = sbuf[d0 + 3],
+                       x4 = sbuf[d0 + 4];
+        o = make_uint4((x0 >> 16) | (x1 << 16), (x1 >> 16) | (x2 << 16), (x2 >> 16) | (x3 << 16),
+                       (x3 >> 16) | (x4 << 16));
+      }
+      *reinterpret_cast<uint4*>(out + g) = o;
+    } else {
+      const uint64_t lo = g > G0 ? g : G0;
+      const uint64_t hi = (g + 16) < G1 ? (g + 16) : G1;
+      for (uint64_t b = lo; b < hi; b += 2)
+        *reinterpret_cast<uint16_t*>(out + b) = s16[(b - G0) >> 1];
+    }
+  }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // ---------------------------------------------------------------------------
 // K1
 // ---------------------------------------------------------------------------
 // ABL: timing-only ablation bits (0 in every product launch; see tools/ablate.py)
 //   1 no look-back, 2 no record stores, 4 no header loads, 8 no index loads,
 //   16 no side outputs
-template <int FPL, bool FLOWS, int PROBE_AUX, int ABL = 0>
+// STAGE 0: the whole tile's records staged in LDS, stored by the block after the
+// look-back; STAGE 1: each wave stages and stores its own 64-record group per
+// round (its records are contiguous in the output), 4.7 KB of LDS per wave.
+template <int FPL, bool FLOWS, int PROBE_AUX, int ABL = 0, int STAGE = 0>
 __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   constexpr int TILE = kBlock * FPL;
-  constexpr int SREC_DW = (TILE * kRecBytes + 32) / 4;
+  constexpr int WBUF_DW = (64 * kRecBytes + 32) / 4;
+  constexpr int SREC_DW = STAGE ? 4 * WBUF_DW : (TILE * kRecBytes + 32) / 4;
   __shared__ __attribute__((aligned(16))) uint32_t s_rec[SREC_DW];
   __shared__ uint32_t s_wcnt[FPL][4];
   __shared__ uint64_t s_excl;
@@ -400,24 +493,37 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   uint64_t fs_seen[FPL];
   uint64_t K[FPL][5];
 
-  // phase A: every frame of the lane is loaded and parsed (loads in flight together)
+  // phase A: index loads of all the lane's frames, then all their header-window
+  // loads (in flight together), then the parse
+  uint64_t offv[FPL], tsv[FPL];
 #pragma unroll
   for (int f = 0; f < FPL; ++f) {
     const uint64_t i = i0 + (uint64_t)f * kBlock + tid;
     acc[f] = false;
     slot[f] = 0xFFFFFFFFu;
     hsh[f] = 0;
-    clen[f] = 0;
     fs_seen[f] = ~0ull;
 #pragma unroll
     for (int j = 0; j < 5; ++j) K[f][j] = 0;
-    if (i < a.n) {
-      const uint64_t off = (ABL & 8) ? i * 64 : a.offset[i];
-      clen[f] = (ABL & 8) ? 64u : a.caplen[i];
-      const uint64_t ts = (ABL & 8) ? i : a.ts[i];
-      acc[f] = parse_frame<(ABL & 4) != 0>(a.arena, a.arena_len, off, clen[f], ts, a.filter_port,
-                                          R[f], K[f]);
-    }
+    const bool in = i < a.n;
+    const uint64_t ic = in ? i : a.n - 1;  // loads stay unconditional (no branch per frame)
+    const uint64_t o = (ABL & 8) ? ic * 64 : a.offset[ic];
+    const uint32_t l = (ABL & 8) ? 64u : a.caplen[ic];
+    const uint64_t t = (ABL & 8) ? ic : a.ts[ic];
+    offv[f] = in ? o : 0;
+    clen[f] = in ? l : 0;
+    tsv[f] = t;
+  }
+  uint32_t lenc[FPL];
+#pragma unroll
+  for (int f = 0; f < FPL; ++f) lenc[f] = clamp_caplen(offv[f], clen[f], a.arena_len);
+  {
+    uint32_t W[FPL][24];
+    load_windows<FPL, (ABL & 4) != 0>(a.arena, a.arena_len, offv, lenc, W);
+#pragma unroll
+    for (int f = 0; f < FPL; ++f)
+      acc[f] = parse_window<(ABL & 4) != 0>(a.arena, a.arena_len, offv[f], lenc[f], tsv[f],
+                                            a.filter_port, W[f], R[f], K[f]);
   }
 #pragma unroll
   for (int f = 0; f < FPL; ++f) {
@@ -505,9 +611,11 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
     }
   }
   if (!(ABL & 2)) {
+    if (STAGE == 0) {
 #pragma unroll
-    for (int f = 0; f < FPL; ++f)
-      if (acc[f]) lds_put_record(s_rec, rank[f] * kRecBytes, R[f]);
+      for (int f = 0; f < FPL; ++f)
+        if (acc[f]) lds_put_record(s_rec, rank[f] * kRecBytes, R[f]);
+    }
   } else {
 #pragma unroll
     for (int f = 0; f < FPL; ++f)
@@ -524,34 +632,27 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   if (tid == 0 && tile == a.ntiles - 1) a.batch->n_acc = excl + total;
 
   // ---- records: LDS -> HBM, 16-B stores, partial chunks as 2-B stores ----
-  const uint64_t wr_lo = excl < a.out_cap ? excl : a.out_cap;
-  const uint64_t wr_hi = (excl + total) < a.out_cap ? (excl + total) : a.out_cap;
-  if (!(ABL & 2) && wr_hi > wr_lo) {
-    const uint64_t G0 = wr_lo * kRecBytes, G1 = wr_hi * kRecBytes;
-    const uint64_t A = G0 & ~15ull;
-    const uint32_t head = (uint32_t)(G0 & 15u);
-    const uint32_t nchunks = (uint32_t)((G1 - A + 15) >> 4);
-    const uint16_t* s16 = reinterpret_cast<const uint16_t*>(s_rec);
-    for (uint32_t c = tid; c < nchunks; c += kBlock) {
-      const uint64_t g = A + 16ull * c;
-      if (g >= G0 && g + 16 <= G1) {
-        const uint32_t sb = 16u * c - head;
-        const uint32_t d0 = sb >> 2;
-        uint4 o;
-        if ((sb & 3u) == 0) {
-          o = make_uint4(s_rec[d0], s_rec[d0 + 1], s_rec[d0 + 2], s_rec[d0 + 3]);
-        } else {
-          const uint32_t x0 = s_rec[d0], x1 = s_rec[d0 + 1], x2 = s_rec[d0 + 2],
-                         x3 = s_rec[d0 + 3], x4 = s_rec[d0 + 4];
-          o = make_uint4((x0 >> 16) | (x1 << 16), (x1 >> 16) | (x2 << 16),
-                         (x2 >> 16) | (x3 << 16), (x3 >> 16) | (x4 << 16));
+  if (!(ABL & 2)) {
+    if (STAGE == 0) {
+      const uint64_t wr_lo = excl < a.out_cap ? excl : a.out_cap;
+      const uint64_t wr_hi = (excl + total) < a.out_cap ? (excl + total) : a.out_cap;
+      if (wr_hi > wr_lo) copy_out(a.out_rec, wr_lo * kRecBytes, wr_hi * kRecBytes, s_rec, tid, kBlock);
+    } else {
+      uint32_t* wbuf = s_rec + wave * WBUF_DW;
+#pragma unroll
+      for (int f = 0; f < FPL; ++f) {
+        const uint64_t b = __ballot(acc[f]);
+        const uint32_t lrank = (uint32_t)__popcll(b & lanemask_lt());
+        const uint64_t g0 = excl + rank[f] - lrank;  // this wave's group start
+        const uint64_t g1 = g0 + (uint64_t)__popcll(b);
+        const uint64_t lo = g0 < a.out_cap ? g0 : a.out_cap;
+        const uint64_t hi = g1 < a.out_cap ? g1 : a.out_cap;
+        if (hi > lo) {
+          if (acc[f]) lds_put_record(wbuf, lrank * kRecBytes, R[f]);
+          wave_lds_sync();
+          copy_out(a.out_rec, lo * kRecBytes, hi * kRecBytes, wbuf, lane, 64);
+          wave_lds_sync();
         }
-        *reinterpret_cast<uint4*>(a.out_rec + g) = o;
-      } else {
-        const uint64_t lo = g > G0 ? g : G0;
-        const uint64_t hi = (g + 16) < G1 ? (g + 16) : G1;
-        for (uint64_t b = lo; b < hi; b += 2)
-          *reinterpret_cast<uint16_t*>(a.out_rec + b) = s16[(b - G0) >> 1];
       }
     }
   }
@@ -701,7 +802,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   const uint64_t n_acc = c.batch->n_acc;
   const uint64_t nflows = c.persist->flow_count + c.batch->n_new;
   const bool use_lds = nflows <= (uint64_t)kCountBins;
-  const uint64_t per = ((n_acc + gridDim.x - 1) / gridDim.x + kCountBlock - 1) / kCountBlock * kCountBlock;
+  const uint64_t per = ((n_acc + gridDim.x - 1) / gridDim.x + 4 * kCountBlock - 1) / (4 * kCountBlock) * (4 * kCountBlock);
   const uint64_t lo = (uint64_t)blockIdx.x * per;
   const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
   if (use_lds) {
@@ -722,52 +823,72 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
     __syncthreads();
   };
   uint64_t running = 0;  // bytes added to the bins since the last flush (block-uniform)
-  for (uint64_t base = lo; base < hi; base += kCountBlock) {
-    const uint64_t p = base + tid;
-    const bool valid = p < hi;
-    const uint32_t s = valid ? c.acc_slot[p] : 0xFFFFFFFFu;
-    const uint32_t len = valid ? c.acc_len[p] : 0u;
-    const uint32_t id = s == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(c.meta[8ull * s + 7] - 1);
-    if (c.out_id && valid && p < c.out_cap) c.out_id[p] = id;
-    const bool mine = id != 0xFFFFFFFFu;
-    const uint64_t am = __ballot(mine);
-    const uint32_t leader = am ? (uint32_t)__ffsll((unsigned long long)am) - 1 : 0u;
-    const uint32_t id0 = __shfl(id, leader);
-    const bool uniform = __all(!mine || id == id0);
-    if (!use_lds) {
-      if (uniform) {
-        const uint64_t bs = wave_sum64(mine ? (uint64_t)len : 0ull);
+  constexpr int U = 4;    // records per thread per iteration (loads issued together)
+  for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
+    uint32_t s[U], len[U], id[U];
+    bool valid[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
+      valid[k] = p < hi;
+      const uint64_t pc = valid[k] ? p : lo;  // unconditional loads
+      s[k] = c.acc_slot[pc];
+      len[k] = c.acc_len[pc];
+      if (!valid[k]) s[k] = 0xFFFFFFFFu, len[k] = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(c.meta[8ull * s[k] + 7] - 1);
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
+      if (c.out_id && valid[k] && p < c.out_cap) c.out_id[p] = id[k];
+    }
+    uint64_t mysum = 0;
+#pragma unroll
+    for (int k = 0; k < U; ++k) mysum += id[k] != 0xFFFFFFFFu ? len[k] : 0u;
+    if (use_lds) {
+      const uint64_t ws = wave_sum64(mysum);
+      if (lane == 0) s_red[wave] = ws;
+      __syncthreads();
+      uint64_t chunk = 0;
+#pragma unroll
+      for (int w = 0; w < kCountBlock / 64; ++w) chunk += s_red[w];
+      if (running + chunk >= 0xFFFFFFFFull) {  // block-uniform decision
+        flush();
+        running = 0;
+      }
+      running += chunk;
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const bool mine = id[k] != 0xFFFFFFFFu;
+      const uint64_t am = __ballot(mine);
+      const uint32_t leader = am ? (uint32_t)__ffsll((unsigned long long)am) - 1 : 0u;
+      const uint32_t id0 = __shfl(id[k], leader);
+      const bool uniform = __all(!mine || id[k] == id0);
+      const uint64_t bs = uniform ? wave_sum64(mine ? (uint64_t)len[k] : 0ull) : 0ull;
+      if (!use_lds) {
+        if (uniform) {
+          if (am && lane == leader) {
+            atomicAdd((unsigned long long*)&c.cnt[2ull * id0], (unsigned long long)__popcll(am));
+            atomicAdd((unsigned long long*)&c.cnt[2ull * id0 + 1], (unsigned long long)bs);
+          }
+        } else if (mine) {
+          atomicAdd((unsigned long long*)&c.cnt[2ull * id[k]], 1ull);
+          atomicAdd((unsigned long long*)&c.cnt[2ull * id[k] + 1], (unsigned long long)len[k]);
+        }
+      } else if (uniform) {
         if (am && lane == leader) {
-          atomicAdd((unsigned long long*)&c.cnt[2ull * id0], (unsigned long long)__popcll(am));
-          atomicAdd((unsigned long long*)&c.cnt[2ull * id0 + 1], (unsigned long long)bs);
+          atomicAdd(&s_pk[id0], (uint32_t)__popcll(am));
+          atomicAdd(&s_by[id0], (uint32_t)bs);
         }
       } else if (mine) {
-        atomicAdd((unsigned long long*)&c.cnt[2ull * id], 1ull);
-        atomicAdd((unsigned long long*)&c.cnt[2ull * id + 1], (unsigned long long)len);
+        atomicAdd(&s_pk[id[k]], 1u);
+        atomicAdd(&s_by[id[k]], len[k]);
       }
-      continue;
     }
-    const uint64_t ws = wave_sum64(mine ? (uint64_t)len : 0ull);
-    if (lane == 0) s_red[wave] = ws;
-    __syncthreads();
-    uint64_t chunk = 0;
-#pragma unroll
-    for (int w = 0; w < kCountBlock / 64; ++w) chunk += s_red[w];
-    if (running + chunk >= 0xFFFFFFFFull) {  // block-uniform decision
-      flush();
-      running = 0;
-    }
-    running += chunk;
-    if (uniform) {
-      if (am && lane == leader) {
-        atomicAdd(&s_pk[id0], (uint32_t)__popcll(am));
-        atomicAdd(&s_by[id0], (uint32_t)ws);
-      }
-    } else if (mine) {
-      atomicAdd(&s_pk[id], 1u);
-      atomicAdd(&s_by[id], len);
-    }
-    __syncthreads();  // s_red reuse
+    if (use_lds) __syncthreads();  // s_red reuse
   }
   if (use_lds) flush();
 }
@@ -928,6 +1049,15 @@ static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s
       default: break;
     }
 #undef TCBEE_ABL_CASE
+  }
+  static const int stage = [] {
+    const char* e = getenv("TCBEE_STAGE");
+    return e ? atoi(e) : 0;
+  }();
+  if (stage == 1) {
+    if (flows) hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1>), grid, dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain, 0, 1>), grid, dim3(kBlock), 0, s, a);
+    return hipGetLastError();
   }
   if (flows) {
     if (aux == kAuxSc1) hipLaunchKernelGGL((k_parse<FPL, true, kAuxSc1>), grid, dim3(kBlock), 0, s, a);
