@@ -323,7 +323,8 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     k.persist = c->d_persist;
     k.meta = c->tab.meta;
     k.cnt = c->tab.cnt;
-    const uint64_t want = (in->n + 16 * kCountBlock - 1) / (16 * kCountBlock);
+    // a block should see many records per flow bin before it flushes its bins
+    const uint64_t want = (in->n + 65535) / 65536;
     const unsigned grid = (unsigned)(want < (uint64_t)c->n_cu ? (want ? want : 1) : c->n_cu);
     TRY_HIP(launch_count(k, grid, s));
   }

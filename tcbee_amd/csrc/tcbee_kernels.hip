@@ -82,6 +82,19 @@ __device__ __forceinline__ uint32_t clamp_caplen(uint64_t off, uint32_t caplen, 
   return caplen > arena_len - off ? (uint32_t)(arena_len - off) : caplen;
 }
 
+// streaming (non-temporal) access helpers: NT=true keeps the once-touched frame
+// stream and record stream from evicting the flow table's lines out of L2
+template <bool NT, class T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT, class T>
+__device__ __forceinline__ void st_stream(T* p, T v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 __device__ __forceinline__ void put_chunk(uint32_t (&w)[24], int c, uint4 v) {
   w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
 }
@@ -91,7 +104,7 @@ __device__ __forceinline__ void put_chunk(uint32_t (&w)[24], int c, uint4 v) {
 // arena (the common case) all FPL x 5 loads are issued unconditionally, back to
 // back; otherwise each lane loads only the chunks of [off, off+min(len,54)),
 // bounds-checked. Chunk 5 (IPv6 tail) is loaded later, for IPv6 frames only.
-template <int FPL, bool NOLOAD>
+template <int FPL, bool NOLOAD, bool NT = false>
 __device__ __forceinline__ void load_windows(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                              const uint64_t (&off)[FPL], const uint32_t (&len)[FPL],
                                              uint32_t (&w)[FPL][24]) {
@@ -118,9 +131,12 @@ __device__ __forceinline__ void load_windows(const uint8_t* __restrict__ arena, 
   if (__all(inb)) {
 #pragma unroll
     for (int f = 0; f < FPL; ++f) {
-      const uint4* src = reinterpret_cast<const uint4*>(arena + (off[f] & ~15ull));
+      const u32x4* src = reinterpret_cast<const u32x4*>(arena + (off[f] & ~15ull));
 #pragma unroll
-      for (int c = 0; c < 5; ++c) put_chunk(w[f], c, src[c]);
+      for (int c = 0; c < 5; ++c) {
+        const u32x4 v = ld_stream<NT>(src + c);
+        put_chunk(w[f], c, make_uint4(v[0], v[1], v[2], v[3]));
+      }
     }
   } else {
 #pragma unroll
@@ -261,9 +277,20 @@ __device__ __forceinline__ bool parse_window(const uint8_t* __restrict__ arena, 
 // read the key by agent-scope loads; a mismatch is re-checked at the coherence
 // point before the probe moves on (never a duplicate flow).
 // ---------------------------------------------------------------------------
+// first_seen word while a flow's first record index is not known yet: the
+// claimer stores kFsFlag | its frame index with the key, so later readers of a
+// hot new flow can tell locally whether they precede the claimer (and only
+// those contend on the atomicMin) instead of all seeing "unset".
+constexpr uint64_t kFsFlag = 1ull << 63;
+
+__device__ __forceinline__ bool fs_needs_min(uint64_t fs_seen, uint64_t frame_i, uint64_t gidx) {
+  if (fs_seen & kFsFlag) return (fs_seen & ~kFsFlag) >= frame_i;  // the claimer or earlier
+  return gidx < fs_seen;
+}
+
 __device__ uint32_t flow_upsert(const FlowTable& T, const uint64_t (&K)[5], uint64_t h,
                                 BatchState* batch, uint64_t* new_list, PersistState* persist,
-                                uint64_t& fs_seen) {
+                                uint64_t& fs_seen, uint64_t claim_mark = ~0ull) {
   const uint64_t tag = hash_tag(h);
   uint64_t s = h & T.mask;
   for (uint64_t probe = 0; probe <= T.mask; ++probe) {
@@ -275,11 +302,12 @@ __device__ uint32_t flow_upsert(const FlowTable& T, const uint64_t (&K)[5], uint
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
 #pragma unroll
         for (int j = 0; j < 5; ++j) st_agent(m + 1 + j, K[j]);
+        st_agent(m + 6, claim_mark);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         st_agent(m, tag);
         const uint64_t slot_no = atomicAdd((unsigned long long*)&batch->n_new, 1ull);
         new_list[slot_no] = s;
-        fs_seen = ~0ull;
+        fs_seen = claim_mark;
         return (uint32_t)s;
       }
       cur = expected;
@@ -429,6 +457,7 @@ __device__ uint32_t tile_accept_count(const ParseArgs& a, uint64_t tile) {
 // Copies staged records [G0, G1) (global byte range; sbuf byte 0 = global byte G0)
 // to out: 16-B stores for whole chunks, 2-B stores for the partial chunks at the
 // ends (bytes there belong to neighbouring groups). Threads t0, t0+step, ...
+template <bool NT = false>
 __device__ __forceinline__ void copy_out(uint8_t* __restrict__ out, uint64_t G0, uint64_t G1,
                                          const uint32_t* sbuf, uint32_t t0, uint32_t step) {
   const uint64_t A = G0 & ~15ull;
@@ -449,7 +478,9 @@ __device__ __forceinline__ void copy_out(uint8_t* __restrict__ out, uint64_t G0,
         o = make_uint4((x0 >> 16) | (x1 << 16), (x1 >> 16) | (x2 << 16), (x2 >> 16) | (x3 << 16),
                        (x3 >> 16) | (x4 << 16));
       }
-      *reinterpret_cast<uint4*>(out + g) = o;
+      u32x4 ov;
+      ov[0] = o.x; ov[1] = o.y; ov[2] = o.z; ov[3] = o.w;
+      st_stream<NT>(reinterpret_cast<u32x4*>(out + g), ov);
     } else {
       const uint64_t lo = g > G0 ? g : G0;
       const uint64_t hi = (g + 16) < G1 ? (g + 16) : G1;
@@ -473,7 +504,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // STAGE 0: the whole tile's records staged in LDS, stored by the block after the
 // look-back; STAGE 1: each wave stages and stores its own 64-record group per
 // round (its records are contiguous in the output), 4.7 KB of LDS per wave.
-template <int FPL, bool FLOWS, int PROBE_AUX, int ABL = 0, int STAGE = 0>
+template <int FPL, bool FLOWS, int PROBE_AUX, int ABL = 0, int STAGE = 0, bool NT = false>
 __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   constexpr int TILE = kBlock * FPL;
   constexpr int WBUF_DW = (64 * kRecBytes + 32) / 4;
@@ -507,9 +538,9 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
     for (int j = 0; j < 5; ++j) K[f][j] = 0;
     const bool in = i < a.n;
     const uint64_t ic = in ? i : a.n - 1;  // loads stay unconditional (no branch per frame)
-    const uint64_t o = (ABL & 8) ? ic * 64 : a.offset[ic];
-    const uint32_t l = (ABL & 8) ? 64u : a.caplen[ic];
-    const uint64_t t = (ABL & 8) ? ic : a.ts[ic];
+    const uint64_t o = (ABL & 8) ? ic * 64 : ld_stream<NT>(a.offset + ic);
+    const uint32_t l = (ABL & 8) ? 64u : ld_stream<NT>(a.caplen + ic);
+    const uint64_t t = (ABL & 8) ? ic : ld_stream<NT>(a.ts + ic);
     offv[f] = in ? o : 0;
     clen[f] = in ? l : 0;
     tsv[f] = t;
@@ -519,7 +550,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   for (int f = 0; f < FPL; ++f) lenc[f] = clamp_caplen(offv[f], clen[f], a.arena_len);
   {
     uint32_t W[FPL][24];
-    load_windows<FPL, (ABL & 4) != 0>(a.arena, a.arena_len, offv, lenc, W);
+    load_windows<FPL, (ABL & 4) != 0, NT>(a.arena, a.arena_len, offv, lenc, W);
 #pragma unroll
     for (int f = 0; f < FPL; ++f)
       acc[f] = parse_window<(ABL & 4) != 0>(a.arena, a.arena_len, offv[f], lenc[f], tsv[f],
@@ -598,7 +629,8 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
           sl = (uint32_t)(h[f] & a.tab.mask);
           fs = W[f][6];
         } else {
-          sl = flow_upsert(a.tab, K[f], h[f], a.batch, a.new_list, a.persist, fs);
+          sl = flow_upsert(a.tab, K[f], h[f], a.batch, a.new_list, a.persist, fs,
+                           kFsFlag | (i0 + (uint64_t)f * kBlock + tid));
         }
       }
       if (uni[f]) {
@@ -636,7 +668,8 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
     if (STAGE == 0) {
       const uint64_t wr_lo = excl < a.out_cap ? excl : a.out_cap;
       const uint64_t wr_hi = (excl + total) < a.out_cap ? (excl + total) : a.out_cap;
-      if (wr_hi > wr_lo) copy_out(a.out_rec, wr_lo * kRecBytes, wr_hi * kRecBytes, s_rec, tid, kBlock);
+      if (wr_hi > wr_lo)
+        copy_out<NT>(a.out_rec, wr_lo * kRecBytes, wr_hi * kRecBytes, s_rec, tid, kBlock);
     } else {
       uint32_t* wbuf = s_rec + wave * WBUF_DW;
 #pragma unroll
@@ -650,7 +683,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
         if (hi > lo) {
           if (acc[f]) lds_put_record(wbuf, lrank * kRecBytes, R[f]);
           wave_lds_sync();
-          copy_out(a.out_rec, lo * kRecBytes, hi * kRecBytes, wbuf, lane, 64);
+          copy_out<NT>(a.out_rec, lo * kRecBytes, hi * kRecBytes, wbuf, lane, 64);
           wave_lds_sync();
         }
       }
@@ -664,10 +697,10 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   for (int f = 0; f < FPL; ++f) {
     const uint64_t p = excl + rank[f];
     if (acc[f] && !(ABL & 16)) {
-      if (a.out_hash && p < a.out_cap) a.out_hash[p] = hsh[f];
+      if (a.out_hash && p < a.out_cap) st_stream<NT>(a.out_hash + p, hsh[f]);
       if (FLOWS) {
-        a.acc_slot[p] = slot[f];
-        a.acc_len[p] = clen[f];
+        st_stream<NT>(a.acc_slot + p, slot[f]);
+        st_stream<NT>(a.acc_len + p, clen[f]);
       }
     }
     if (FLOWS) {
@@ -677,11 +710,12 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
         const uint32_t leader = (uint32_t)__ffsll((unsigned long long)am) - 1;
         const uint32_t s0 = __shfl(slot[f], leader);
         const uint64_t gidx = rec_base + p;
+        const uint64_t frame_i = i0 + (uint64_t)f * kBlock + tid;
         if (__all(!mine || slot[f] == s0)) {
           // leader = lowest rank of the wave = its smallest accepted index
-          if (lane == leader && gidx < fs_seen[f])
+          if (lane == leader && fs_needs_min(fs_seen[f], frame_i, gidx))
             atomicMin((unsigned long long*)&a.tab.meta[8ull * s0 + 6], (unsigned long long)gidx);
-        } else if (mine && gidx < fs_seen[f]) {
+        } else if (mine && fs_needs_min(fs_seen[f], frame_i, gidx)) {
           atomicMin((unsigned long long*)&a.tab.meta[8ull * slot[f] + 6], (unsigned long long)gidx);
         }
       }
@@ -1057,6 +1091,15 @@ static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s
   if (stage == 1) {
     if (flows) hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1>), grid, dim3(kBlock), 0, s, a);
     else hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain, 0, 1>), grid, dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+  }
+  static const int nt = [] {
+    const char* e = getenv("TCBEE_NT");
+    return e ? atoi(e) : 0;
+  }();
+  if (nt) {
+    if (flows) hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 0, true>), grid, dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain, 0, 0, true>), grid, dim3(kBlock), 0, s, a);
     return hipGetLastError();
   }
   if (flows) {

@@ -57,6 +57,7 @@ def main():
             for v in variants:
                 p = parsers[v]
                 def step():
+                    p.reset_flows(stream=stream, sync=False)  # one fresh trace per step, as bench.py
                     p.parse_device(d_arena, alen, d_off, d_len, d_ts, n, d_rec, n,
                                    d_hash if v[1] else None, d_id if v[1] else None, d_n, d_ctr,
                                    flows=v[1], stream=stream)
