@@ -19,6 +19,7 @@ struct tcbee_ctx {
   hipStream_t stream = nullptr;
   uint64_t max_frames = 0, max_arena = 0, max_flows = 0;
   int fpl = 2;
+  bool reset_pending = false;   // tcbee_flow_reset_device: applied by the next launch
   uint32_t withhold_every = 0;  // TCBEE_TEST_WITHHOLD (look-back recount test hook)
 
   FlowTable tab{};
@@ -123,6 +124,7 @@ const char* tcbee_strerror(int code) {
     case TCBEE_EIO: return "I/O error";
     case TCBEE_EFORMAT: return "malformed input";
     case TCBEE_ESPIN: return "in-kernel wait timed out";
+    case TCBEE_EDB: return "database statement failed";
     default: return "unknown error";
   }
 }
@@ -241,17 +243,26 @@ int tcbee_flow_reset(tcbee_ctx* c) {
   TRY_HIP(launch_table_init(c->tab, c->stream));
   TRY_HIP(hipMemsetAsync(c->d_persist, 0, sizeof(PersistState), c->stream));
   TRY_HIP(hipStreamSynchronize(c->stream));
+  c->reset_pending = false;
   return TCBEE_OK;
 }
 
 int tcbee_flow_reset_device(tcbee_ctx* c, void* stream) {
   if (!c) return TCBEE_EINVAL;
-  TRY_HIP(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  TRY_HIP(launch_table_init(c->tab, s));
-  TRY_HIP(hipMemsetAsync(c->d_persist, 0, sizeof(PersistState), s));
+  (void)stream;  // folded into the next parse's prep kernel (or applied before a table read)
+  c->reset_pending = true;
   return TCBEE_OK;
 }
+
+namespace {
+int apply_pending_reset(tcbee_ctx* c, hipStream_t s) {
+  if (!c->reset_pending) return TCBEE_OK;
+  TRY_HIP(launch_table_init(c->tab, s));
+  TRY_HIP(hipMemsetAsync(c->d_persist, 0, sizeof(PersistState), s));
+  c->reset_pending = false;
+  return TCBEE_OK;
+}
+}  // namespace
 
 int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_cfg* cfg,
                              uint8_t* out_rec74, uint64_t out_cap, uint32_t* out_flow_hash,
@@ -267,12 +278,23 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
   const bool flows = (cfg->flags & TCBEE_F_NO_FLOWS) == 0;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   TRY_HIP(hipSetDevice(c->device));
-  TRY_HIP(hipMemsetAsync(c->d_batch, 0, sizeof(BatchState), s));
-
   const int fpl = c->fpl;
   const uint64_t ntiles = (in->n + tile_frames(fpl) - 1) / tile_frames(fpl);
+  const uint64_t nwords = flows && ntiles ? (in->n + 31) / 32 : 0;
+  {
+    PrepArgs pa{};
+    pa.batch = c->d_batch;
+    pa.tile_status = c->d_tile_status;
+    pa.ntiles = ntiles;
+    pa.bitmap = c->d_bitmap;
+    pa.nwords = nwords;
+    pa.reset = c->reset_pending;
+    pa.tab = c->tab;
+    pa.persist = c->d_persist;
+    TRY_HIP(launch_prep(pa, s));
+    c->reset_pending = false;
+  }
   if (ntiles > 0) {
-    TRY_HIP(hipMemsetAsync(c->d_tile_status, 0, ntiles * sizeof(uint64_t), s));
     ParseArgs a{};
     a.arena = in->arena;
     a.arena_len = in->arena_len;
@@ -310,11 +332,14 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     r.bitmap = c->d_bitmap;
     r.wprefix = c->d_wprefix;
     r.bprefix = c->d_bprefix;
-    r.nwords = (in->n + 31) / 32;
+    r.nwords = nwords;
     r.nblocks = (r.nwords + kScanWordsPerBlock - 1) / kScanWordsPerBlock;
-    TRY_HIP(hipMemsetAsync(c->d_bitmap, 0, r.nwords * sizeof(uint32_t), s));
     TRY_HIP(launch_rank(r, s));
     CountArgs k{};
+    k.out_n = out_n_dev;
+    k.ctr = ctr_dev;
+    k.direction = cfg->direction;
+    k.persist_rw = c->d_persist;
     k.acc_slot = c->d_slot_scratch;
     k.acc_len = c->d_len_scratch;
     k.out_id = out_flow_id;
@@ -323,12 +348,14 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     k.persist = c->d_persist;
     k.meta = c->tab.meta;
     k.cnt = c->tab.cnt;
-    // a block should see many records per flow bin before it flushes its bins
-    const uint64_t want = (in->n + 65535) / 65536;
+    // trade-off: more blocks = more latency hidden; each block flushes every bin it
+    // touched, so a block should see a few thousand records
+    const uint64_t want = (in->n + 8191) / 8192;
     const unsigned grid = (unsigned)(want < (uint64_t)c->n_cu ? (want ? want : 1) : c->n_cu);
-    TRY_HIP(launch_count(k, grid, s));
+    TRY_HIP(launch_count(k, grid, s));  // finalize is folded into its block 0
+  } else {
+    TRY_HIP(launch_finalize(c->d_batch, c->d_persist, out_cap, out_n_dev, ctr_dev, cfg->direction, s));
   }
-  TRY_HIP(launch_finalize(c->d_batch, c->d_persist, out_cap, out_n_dev, ctr_dev, cfg->direction, s));
   return TCBEE_OK;
 }
 
@@ -383,6 +410,7 @@ int tcbee_parse_batch(tcbee_ctx* c, const tcbee_frames* in, const tcbee_cfg* cfg
 int tcbee_flow_count(tcbee_ctx* c, uint64_t* n) {
   if (!c || !n) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
+  if (int rc = apply_pending_reset(c, c->stream)) return rc;
   PersistState p{};
   TRY_HIP(hipMemcpyAsync(&p, c->d_persist, sizeof(p), hipMemcpyDeviceToHost, c->stream));
   TRY_HIP(hipStreamSynchronize(c->stream));
@@ -393,6 +421,7 @@ int tcbee_flow_count(tcbee_ctx* c, uint64_t* n) {
 int tcbee_flow_export(tcbee_ctx* c, tcbee_flow_entry* out, uint64_t cap, uint64_t* n) {
   if (!c || !n || (cap && !out)) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
+  if (int rc = apply_pending_reset(c, c->stream)) return rc;
   std::vector<uint64_t> meta, cnt;
   try {
     meta.resize(8 * c->nslots);
@@ -428,6 +457,7 @@ int tcbee_flow_export_device(tcbee_ctx* c, tcbee_flow_entry* out_dev, uint64_t c
   if (!c || (cap && !out_dev)) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (int rc = apply_pending_reset(c, s)) return rc;
   TRY_HIP(launch_export(c->tab, reinterpret_cast<uint64_t*>(out_dev), cap, c->d_persist, n_dev, s));
   return TCBEE_OK;
 }
@@ -457,6 +487,7 @@ int tcbee_flow_merge_device(tcbee_ctx* c, const tcbee_flow_entry* ent_dev, uint6
     c->m_words = words;
   }
   // fresh table: the merge result replaces whatever this context held
+  c->reset_pending = false;
   TRY_HIP(launch_table_init(c->tab, s));
   TRY_HIP(hipMemsetAsync(c->d_persist, 0, sizeof(PersistState), s));
   TRY_HIP(hipMemsetAsync(c->d_batch, 0, sizeof(BatchState), s));

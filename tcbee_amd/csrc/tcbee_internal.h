@@ -34,13 +34,24 @@ struct PersistState {
 
 // Zeroed before every batch (one 32-B memset).
 struct BatchState {
-  uint64_t n_acc;   // accepted frames in this batch (last tile writes it)
-  uint64_t n_new;   // flows first claimed in this batch
-  uint32_t pad0;
-  uint32_t pad2;
+  uint64_t n_acc;       // accepted frames in this batch (last tile writes it)
+  uint64_t n_new;       // flows first claimed in this batch
+  uint64_t flow_total;  // flows with ids after this batch (rank step writes it)
   uint64_t pad1;
 };
 static_assert(sizeof(BatchState) == 32, "memset size");
+
+struct PrepArgs {
+  BatchState* batch;
+  uint64_t* tile_status;
+  uint64_t ntiles;
+  uint32_t* bitmap;
+  uint64_t nwords;
+  bool reset;           // also empty the flow table (a pending tcbee_flow_reset_device)
+  FlowTable tab;
+  PersistState* persist;
+};
+hipError_t launch_prep(const PrepArgs& p, hipStream_t s);
 
 struct ParseArgs {
   const uint8_t* arena;
@@ -81,6 +92,10 @@ hipError_t launch_table_init(FlowTable t, hipStream_t s);
 hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s);
 hipError_t launch_rank(const RankArgs& r, hipStream_t s);
 struct CountArgs {
+  uint64_t* out_n;           // finalize (block 0): record count, counters, running bases
+  tcbee_counters* ctr;
+  int direction;
+  PersistState* persist_rw;
   const uint32_t* acc_slot;
   const uint32_t* acc_len;
   uint32_t* out_id;
@@ -117,6 +132,7 @@ hipError_t launch_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, 
 
 constexpr int kBlock = 256;
 constexpr int kScanWordsPerBlock = 2048;  // 256 threads x 8 words
+constexpr uint64_t kRankSmallWords = 1024 * 32;  // single-block rank up to 1M frames
 constexpr int kCountBlock = 1024;
 constexpr int kCountBins = 16384;         // 2 x 64 KiB of LDS
 

@@ -740,8 +740,84 @@ __global__ void k_table_init(FlowTable t) {
 }
 
 // ---------------------------------------------------------------------------
+// per-batch preparation in one launch (instead of 3-5 memsets + table init)
+// ---------------------------------------------------------------------------
+__global__ void k_prep(PrepArgs p) {
+  const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  if (t0 < 4) reinterpret_cast<uint64_t*>(p.batch)[t0] = 0;
+  for (uint64_t i = t0; i < p.ntiles; i += stride) p.tile_status[i] = 0;
+  for (uint64_t i = t0; i < p.nwords; i += stride) p.bitmap[i] = 0;
+  if (p.reset) {
+    if (t0 < sizeof(PersistState) / 8) reinterpret_cast<uint64_t*>(p.persist)[t0] = 0;
+    const uint64_t nslots = p.tab.mask + 1;
+    for (uint64_t s = t0; s < nslots; s += stride) {
+      uint64_t* m = p.tab.meta + 8 * s;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = 0;
+      m[6] = ~0ull;
+      p.tab.cnt[2 * s] = 0;
+      p.tab.cnt[2 * s + 1] = 0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // K2: ranks of this batch's new flows by first_seen
 // ---------------------------------------------------------------------------
+// Small batches (nwords <= kRankSmallWords): mark + scan + assign in ONE block.
+__global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
+  __shared__ uint32_t s_tmp[16];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint64_t n_new = r.batch->n_new;
+  const uint64_t base = r.persist->rec_base;
+  const uint64_t fbase = r.persist->flow_count;
+  for (uint64_t j = tid; j < n_new; j += 1024) {
+    const uint64_t local = r.tab.meta[8 * r.new_list[j] + 6] - base;
+    if ((local >> 5) < r.nwords) atomicOr(&r.bitmap[local >> 5], 1u << (local & 31));
+  }
+  __syncthreads();
+  // exclusive popcount prefix per word: thread t owns words [t*wpt, (t+1)*wpt),
+  // wpt <= 64, all loaded into registers at once (independent loads in flight)
+  constexpr int kMaxWpt = (int)(kRankSmallWords / 1024);
+  const uint32_t wpt = (uint32_t)((r.nwords + 1023) / 1024);
+  const uint64_t w0 = (uint64_t)tid * wpt;
+  uint32_t wv[kMaxWpt];
+#pragma unroll
+  for (int k = 0; k < kMaxWpt; ++k)
+    wv[k] = ((uint32_t)k < wpt && w0 + k < r.nwords)
+                ? __hip_atomic_load(&r.bitmap[w0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                : 0u;
+  uint32_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < kMaxWpt; ++k) sum += __popc(wv[k]);
+  uint32_t x = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) s_tmp[wave] = x;
+  __syncthreads();
+  uint32_t pre = x - sum;
+  for (uint32_t w = 0; w < wave; ++w) pre += s_tmp[w];
+#pragma unroll
+  for (int k = 0; k < kMaxWpt; ++k) {
+    if ((uint32_t)k < wpt && w0 + k < r.nwords) r.wprefix[w0 + k] = pre;
+    pre += __popc(wv[k]);
+  }
+  __syncthreads();
+  for (uint64_t j = tid; j < n_new; j += 1024) {
+    const uint64_t s = r.new_list[j];
+    const uint64_t local = r.tab.meta[8 * s + 6] - base;
+    const uint64_t w = local >> 5;
+    const uint32_t below = __hip_atomic_load(&r.bitmap[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+                           ((1u << (local & 31)) - 1u);
+    r.tab.meta[8 * s + 7] = fbase + r.wprefix[w] + __popc(below) + 1;
+  }
+  if (tid == 0) r.batch->flow_total = fbase + n_new;
+}
+
 __global__ void k_mark(RankArgs r) {
   const uint64_t n_new = r.batch->n_new;
   const uint64_t base = r.persist->rec_base;
@@ -820,6 +896,7 @@ __global__ void k_assign(RankArgs r) {
     const uint64_t id = fbase + r.bprefix[w / kScanWordsPerBlock] + r.wprefix[w] + __popc(below);
     r.tab.meta[8 * s + 7] = id + 1;
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) r.batch->flow_total = fbase + n_new;
 }
 
 // K3: per accepted frame, slot -> dense id (written for records p < out_cap) and
@@ -834,7 +911,20 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   __shared__ uint64_t s_red[kCountBlock / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint64_t n_acc = c.batch->n_acc;
-  const uint64_t nflows = c.persist->flow_count + c.batch->n_new;
+  const uint64_t nflows = c.batch->flow_total;
+  if (blockIdx.x == 0 && tid == 0) {
+    // finalize (no other block reads persist in this launch)
+    const uint64_t written = n_acc < c.out_cap ? n_acc : c.out_cap;
+    if (c.out_n) *c.out_n = written;
+    if (c.ctr) {
+      if (c.direction) c.ctr->egress += n_acc;  // EGRESS_EVENTS, tc.rs:167
+      else c.ctr->ingress += n_acc;             // INGRESS_EVENTS, xdp.rs:207
+      c.ctr->handled += written;                // EVENTS_HANDLED, xdp.rs:214
+      c.ctr->dropped += n_acc - written;        // EVENTS_DROPPED, xdp.rs:217
+    }
+    c.persist_rw->rec_base += n_acc;
+    c.persist_rw->flow_count = nflows;
+  }
   const bool use_lds = nflows <= (uint64_t)kCountBins;
   const uint64_t per = ((n_acc + gridDim.x - 1) / gridDim.x + 4 * kCountBlock - 1) / (4 * kCountBlock) * (4 * kCountBlock);
   const uint64_t lo = (uint64_t)blockIdx.x * per;
@@ -1120,7 +1210,18 @@ hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s) 
   }
 }
 
+hipError_t launch_prep(const PrepArgs& p, hipStream_t s) {
+  uint64_t work = p.ntiles > p.nwords ? p.ntiles : p.nwords;
+  if (p.reset && p.tab.mask + 1 > work) work = p.tab.mask + 1;
+  hipLaunchKernelGGL(k_prep, dim3(grid_for(work < 4 ? 4 : work)), dim3(kBlock), 0, s, p);
+  return hipGetLastError();
+}
+
 hipError_t launch_rank(const RankArgs& r, hipStream_t s) {
+  if (r.nwords <= kRankSmallWords) {
+    hipLaunchKernelGGL(k_rank_small, dim3(1), dim3(1024), 0, s, r);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_mark, dim3(1024), dim3(kBlock), 0, s, r);
   hipLaunchKernelGGL(k_scan_words, dim3((unsigned)r.nblocks), dim3(kBlock), 0, s, r);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, r);
