@@ -59,6 +59,7 @@ extern "C" {
 #define TCBEE_EIO                -7  /* file I/O error                          */
 #define TCBEE_EFORMAT            -8  /* malformed input file                    */
 #define TCBEE_ESPIN              -9  /* a bounded in-kernel wait timed out      */
+#define TCBEE_EDB               -10  /* SQLite statement failed (sink)          */
 
 /* ---- directions (which hook / which output file) ------------------------- */
 #define TCBEE_DIR_INGRESS 0  /* xdp_hook  -> xdp.tcp, counts INGRESS_EVENTS */

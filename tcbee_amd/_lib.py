@@ -30,6 +30,7 @@ ENODEV = -6
 EIO = -7
 EFORMAT = -8
 ESPIN = -9
+EDB = -10
 
 
 class TcbeeError(RuntimeError):

@@ -24,6 +24,10 @@ def _ensure_built():
     if not os.path.exists(oracle_so):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
                        stdout=subprocess.DEVNULL)
+    host_so = os.path.join(ROOT, "tcbee_amd", "lib", "libtcbee_host.so")
+    if not os.path.exists(host_so):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "tcbee_amd", "host")], check=True,
+                       stdout=subprocess.DEVNULL)
     lib_so = os.path.join(ROOT, "tcbee_amd", "lib", "libtcbee_amd.so")
     if not os.path.exists(lib_so):
         subprocess.run(["make", "-C", os.path.join(ROOT, "tcbee_amd", "csrc")], check=True,
