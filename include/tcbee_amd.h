@@ -220,6 +220,50 @@ int tcbee_gen_frames_host(uint8_t* arena, const uint64_t* offset,
                           const uint32_t* caplen, uint64_t n, uint64_t first_index,
                           int kind, uint64_t n_flows, uint64_t seed);
 
+/* ---- ingest pipeline: host frames -> records on the host ----------------
+ * (replaces the live ring drain of
+ * tcbee/src/eBPF/probes/headers.rs:67-109.) Frames in pageable host memory (a
+ * pcap mapping, a capture buffer) are gathered chunk by chunk into pinned
+ * staging by `threads` host threads, copied H2D on one stream, parsed on the
+ * pipe's context (flow ids continue across chunks and calls), and the exact
+ * record count copied D2H on a third stream; `depth` chunks are in flight, so
+ * staging, both DMA directions and the kernels overlap.
+ * window == 0: whole frames are shipped. window >= 80 (multiple of 16): only
+ * the first min(caplen, window) bytes of each frame are shipped, with its
+ * original caplen — the record path never reads past byte 74 of a frame, so
+ * outputs are identical, and PCIe carries ~window+12 bytes per frame. */
+typedef struct tcbee_pipe tcbee_pipe;
+typedef struct tcbee_pipe_cfg {
+    uint64_t chunk_frames;  /* frames per chunk (0 = 1<<20)                     */
+    uint64_t chunk_bytes;   /* staged arena bytes per chunk, window == 0 (0 = 512 MiB) */
+    uint32_t window;        /* 0 = whole frames, else header window bytes         */
+    uint32_t depth;         /* chunks in flight, 3..16 (0 = 3)                     */
+    uint32_t threads;       /* host staging threads (0 = 8)                        */
+    uint32_t reserved;
+} tcbee_pipe_cfg;
+typedef struct tcbee_pipe_stats {
+    uint64_t frames, records, chunks;
+} tcbee_pipe_stats;
+/* Called once per chunk, in order, with that chunk's records (pinned host
+ * memory valid during the call); flow_id NULL with TCBEE_F_NO_FLOWS. A
+ * non-zero return aborts the run with that code. */
+typedef int (*tcbee_pipe_sink_fn)(void* user, const uint8_t* rec74, const uint32_t* flow_id,
+                                  uint64_t n, uint64_t first_record);
+
+int tcbee_pipe_create(tcbee_pipe** out, int device, const tcbee_pipe_cfg* cfg,
+                      uint64_t max_flows);
+int tcbee_pipe_destroy(tcbee_pipe* p);
+/* The pipe's context (flow table export / reset, status, profiling). */
+int tcbee_pipe_ctx(tcbee_pipe* p, tcbee_ctx** ctx);
+int tcbee_pipe_get_stats(const tcbee_pipe* p, tcbee_pipe_stats* st);
+/* Synchronous. Records (and flow ids) go to out_rec74 / out_flow_id (host,
+ * may be NULL) and/or to fn. *out_n = records produced; ctr accumulated into.
+ * TCBEE_ECAPACITY if more than out_cap records were produced (the first out_cap
+ * are written). */
+int tcbee_pipe_run(tcbee_pipe* p, const tcbee_frames* in_host, const tcbee_cfg* cfg,
+                   uint8_t* out_rec74, uint64_t out_cap, uint32_t* out_flow_id,
+                   tcbee_pipe_sink_fn fn, void* user, uint64_t* out_n, tcbee_counters* ctr);
+
 /* ---- host utilities (no GPU needed) ------------------------------------- */
 /* tcbee flow hash v1 of a 40-byte key (DESIGN.md "Flow hash"). */
 uint64_t tcbee_flow_hash64(const uint8_t key40[TCBEE_KEY_BYTES]);

@@ -64,7 +64,20 @@ class FlowEntry(C.Structure):
                 ("bytes", C.c_uint64), ("first_seen", C.c_uint64)]
 
 
-assert C.sizeof(Cfg) == 8 and C.sizeof(Frames) == 48
+class PipeCfg(C.Structure):
+    _fields_ = [("chunk_frames", C.c_uint64), ("chunk_bytes", C.c_uint64),
+                ("window", C.c_uint32), ("depth", C.c_uint32), ("threads", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+class PipeStats(C.Structure):
+    _fields_ = [("frames", C.c_uint64), ("records", C.c_uint64), ("chunks", C.c_uint64)]
+
+
+# int (*)(void* user, const uint8_t* rec74, const uint32_t* flow_id, uint64_t n, uint64_t first)
+PIPE_SINK_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64)
+
+assert C.sizeof(Cfg) == 8 and C.sizeof(Frames) == 48 and C.sizeof(PipeCfg) == 32
 assert C.sizeof(Counters) == 32 and C.sizeof(FlowEntry) == 64
 
 # every symbol declared in include/tcbee_amd.h, with its ctypes signature
@@ -104,6 +117,14 @@ _SIGS = {
     "tcbee_gen_frames_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                         C.c_uint64, C.c_int, C.c_uint64, C.c_uint64]),
     "tcbee_flow_hash64": (C.c_uint64, [C.c_void_p]),
+    "tcbee_pipe_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(PipeCfg),
+                                    C.c_uint64]),
+    "tcbee_pipe_destroy": (C.c_int, [C.c_void_p]),
+    "tcbee_pipe_ctx": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
+    "tcbee_pipe_get_stats": (C.c_int, [C.c_void_p, C.POINTER(PipeStats)]),
+    "tcbee_pipe_run": (C.c_int, [C.c_void_p, C.POINTER(Frames), C.POINTER(Cfg), C.c_void_p,
+                                 C.c_uint64, C.c_void_p, PIPE_SINK_FN, C.c_void_p,
+                                 C.POINTER(C.c_uint64), C.POINTER(Counters)]),
 }
 EXPORTED = tuple(_SIGS)
 

@@ -1,0 +1,470 @@
+// tcbee_pipe.hip — host-frames ingest pipeline:
+// frames in host memory (a pcap mapping, a capture ring) -> pinned staging ->
+// H2D -> parse -> D2H -> records on the host, with every stage of chunk i
+// overlapping the others' work on chunks i-1 / i-2:
+//
+//   host threads   stage(i)  ─┐                     consume(i-2)
+//   H2D engine                └─ H2D(i)
+//   compute                            parse(i-1)
+//   D2H engine                                      D2H(i-1)  (exact record count)
+//
+// Staging modes
+//   window == 0  whole frames are gathered back to back (payload included).
+//   window >= 80 "header window": only min(caplen, window) bytes of each frame
+//                are shipped, at stride `window`, with the ORIGINAL caplen. The
+//                record path reads at most 74 bytes of a frame and decides only
+//                on bytes < min(caplen, 74) and on caplen itself (xdp.rs:37-152
+//                read nothing past the TCP header), so the records, flow ids
+//                and counters are identical to shipping whole frames — while
+//                PCIe carries ~92 B per frame instead of the frame size.
+//
+// The live source this replaces is the ring drain of the reference
+// (tcbee/src/eBPF/probes/headers.rs:67-109): there the kernel hands each
+// packet to the hooks; here a batch of recorded frames is streamed through
+// the GPU hooks.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "../../include/tcbee_amd.h"
+
+namespace {
+
+__global__ void k_window_offsets(uint64_t* off, uint64_t n, uint64_t window) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    off[i] = i * window;
+}
+
+int map_err(hipError_t e) {
+  if (e == hipSuccess) return TCBEE_OK;
+  if (e == hipErrorOutOfMemory) return TCBEE_ENOMEM;
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return TCBEE_ENODEV;
+  return TCBEE_EDEVICE;
+}
+
+#define TRY_HIP(expr)                          \
+  do {                                         \
+    hipError_t e_ = (expr);                    \
+    if (e_ != hipSuccess) return map_err(e_);  \
+  } while (0)
+
+// Fixed pool of host threads running one parallel-for at a time.
+class Pool {
+ public:
+  explicit Pool(unsigned n) {
+    for (unsigned i = 1; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
+    n_ = n;
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  unsigned size() const { return n_; }
+  // fn(part, parts) on every thread (the caller is part 0); returns when all are done.
+  void run(const std::function<void(unsigned, unsigned)>& fn) {
+    if (n_ == 1) {
+      fn(0, 1);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      fn_ = &fn;
+      pending_ = n_ - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0, n_);
+    std::unique_lock<std::mutex> lk(m_);
+    done_cv_.wait(lk, [this] { return pending_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void loop(unsigned id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(unsigned, unsigned)>* fn;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+        fn = fn_;
+      }
+      (*fn)(id, n_);
+      {
+        std::lock_guard<std::mutex> g(m_);
+        if (--pending_ == 0) done_cv_.notify_one();
+      }
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(unsigned, unsigned)>* fn_ = nullptr;
+  unsigned n_ = 1, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+struct Slot {
+  // pinned host
+  uint8_t* h_arena = nullptr;
+  uint64_t* h_off = nullptr;
+  uint32_t* h_len = nullptr;
+  uint64_t* h_ts = nullptr;
+  uint8_t* h_rec = nullptr;
+  uint32_t* h_id = nullptr;
+  uint64_t* h_meta = nullptr;  // [0] = records, [1..4] = counters
+  // device
+  uint8_t* d_arena = nullptr;
+  uint64_t* d_off = nullptr;
+  uint32_t* d_len = nullptr;
+  uint64_t* d_ts = nullptr;
+  uint8_t* d_rec = nullptr;
+  uint32_t* d_id = nullptr;
+  uint64_t* d_meta = nullptr;  // same layout as h_meta
+  hipEvent_t ev_h2d = nullptr, ev_parse = nullptr, ev_d2h = nullptr;
+  // chunk bookkeeping
+  uint64_t lo = 0, hi = 0, arena_used = 0, n_rec = 0, first_record = 0;
+};
+
+}  // namespace
+
+struct tcbee_pipe {
+  int device = 0;
+  tcbee_pipe_cfg cfg{};
+  tcbee_ctx* ctx = nullptr;
+  hipStream_t s_h2d = nullptr, s_comp = nullptr, s_d2h = nullptr;
+  std::vector<Slot> slots;
+  Pool* pool = nullptr;
+  tcbee_pipe_stats st{};
+};
+
+namespace {
+
+void free_pipe(tcbee_pipe* p) {
+  if (!p) return;
+  (void)hipSetDevice(p->device);
+  if (p->s_h2d) (void)hipStreamSynchronize(p->s_h2d);
+  if (p->s_d2h) (void)hipStreamSynchronize(p->s_d2h);
+  if (p->ctx) (void)tcbee_ctx_sync(p->ctx);
+  for (Slot& s : p->slots) {
+    for (void* h : {(void*)s.h_arena, (void*)s.h_off, (void*)s.h_len, (void*)s.h_ts,
+                    (void*)s.h_rec, (void*)s.h_id, (void*)s.h_meta})
+      if (h) (void)hipHostFree(h);
+    for (void* d : {(void*)s.d_arena, (void*)s.d_off, (void*)s.d_len, (void*)s.d_ts,
+                    (void*)s.d_rec, (void*)s.d_id, (void*)s.d_meta})
+      if (d) (void)hipFree(d);
+    for (hipEvent_t e : {s.ev_h2d, s.ev_parse, s.ev_d2h})
+      if (e) (void)hipEventDestroy(e);
+  }
+  if (p->s_h2d) (void)hipStreamDestroy(p->s_h2d);
+  if (p->s_d2h) (void)hipStreamDestroy(p->s_d2h);
+  if (p->ctx) tcbee_ctx_destroy(p->ctx);
+  delete p->pool;
+  delete p;
+}
+
+template <class T>
+hipError_t hpin(T** p, uint64_t count) {
+  return hipHostMalloc(reinterpret_cast<void**>(p), (count ? count : 1) * sizeof(T),
+                       hipHostMallocDefault);
+}
+template <class T>
+hipError_t dmal(T** p, uint64_t count) {
+  return hipMalloc(reinterpret_cast<void**>(p), (count ? count : 1) * sizeof(T));
+}
+
+int alloc_slot(tcbee_pipe* p, Slot& s) {
+  const uint64_t F = p->cfg.chunk_frames, B = p->cfg.chunk_bytes;
+  TRY_HIP(hpin(&s.h_arena, B + 64));
+  TRY_HIP(hpin(&s.h_off, F));
+  TRY_HIP(hpin(&s.h_len, F));
+  TRY_HIP(hpin(&s.h_ts, F));
+  TRY_HIP(hpin(&s.h_rec, F * TCBEE_RECORD_BYTES));
+  TRY_HIP(hpin(&s.h_id, F));
+  TRY_HIP(hpin(&s.h_meta, 8));
+  TRY_HIP(dmal(&s.d_arena, B + 64));
+  TRY_HIP(dmal(&s.d_off, F));
+  TRY_HIP(dmal(&s.d_len, F));
+  TRY_HIP(dmal(&s.d_ts, F));
+  TRY_HIP(dmal(&s.d_rec, F * TCBEE_RECORD_BYTES + 64));
+  TRY_HIP(dmal(&s.d_id, F));
+  TRY_HIP(dmal(&s.d_meta, 8));
+  TRY_HIP(hipEventCreateWithFlags(&s.ev_h2d, hipEventDisableTiming));
+  TRY_HIP(hipEventCreateWithFlags(&s.ev_parse, hipEventDisableTiming));
+  TRY_HIP(hipEventCreateWithFlags(&s.ev_d2h, hipEventDisableTiming));
+  return TCBEE_OK;
+}
+
+// Frames [lo, hi) that fit one chunk, starting at lo.
+uint64_t chunk_end(const tcbee_pipe* p, const tcbee_frames* in, uint64_t lo) {
+  const uint64_t F = p->cfg.chunk_frames, B = p->cfg.chunk_bytes;
+  uint64_t hi = lo + F < in->n ? lo + F : in->n;
+  if (p->cfg.window) return hi;  // stride window: F * window <= B by construction
+  uint64_t bytes = 0, i = lo;
+  for (; i < hi; ++i) {
+    if (bytes + in->caplen[i] > B) break;
+    bytes += in->caplen[i];
+  }
+  return i;
+}
+
+// Gather frames [s.lo, s.hi) into the slot's pinned staging (pool-parallel).
+void stage(tcbee_pipe* p, const tcbee_frames* in, Slot& s) {
+  const uint64_t lo = s.lo, n = s.hi - s.lo, W = p->cfg.window;
+  if (W) {
+    p->pool->run([&](unsigned part, unsigned parts) {
+      const uint64_t a = n * part / parts, b = n * (part + 1) / parts;
+      for (uint64_t k = a; k < b; ++k) {
+        const uint64_t f = lo + k;
+        const uint32_t len = in->caplen[f];
+        const uint64_t o = in->offset[f];
+        const uint64_t want = len < W ? len : W;
+        uint64_t cp = want;
+        if (o >= in->arena_len) cp = 0;
+        else if (cp > in->arena_len - o) cp = in->arena_len - o;
+        std::memcpy(s.h_arena + k * W, in->arena + o, cp);
+        if (cp < want) std::memset(s.h_arena + k * W + cp, 0, want - cp);  // past the arena
+        s.h_len[k] = len;
+        s.h_ts[k] = in->ts_ns[f];
+      }
+    });
+    s.arena_used = n * W;
+    return;
+  }
+  // whole frames: exclusive prefix of caplen per part, then copy
+  const unsigned parts = p->pool->size();
+  std::vector<uint64_t> part_bytes(parts + 1, 0);
+  p->pool->run([&](unsigned part, unsigned np) {
+    const uint64_t a = n * part / np, b = n * (part + 1) / np;
+    uint64_t sum = 0;
+    for (uint64_t k = a; k < b; ++k) sum += in->caplen[lo + k];
+    part_bytes[part + 1] = sum;
+  });
+  for (unsigned i = 0; i < parts; ++i) part_bytes[i + 1] += part_bytes[i];
+  p->pool->run([&](unsigned part, unsigned np) {
+    const uint64_t a = n * part / np, b = n * (part + 1) / np;
+    uint64_t pos = part_bytes[part];
+    for (uint64_t k = a; k < b; ++k) {
+      const uint64_t f = lo + k;
+      const uint32_t len = in->caplen[f];
+      const uint64_t o = in->offset[f];
+      uint64_t cp = len;
+      if (o >= in->arena_len) cp = 0;
+      else if (cp > in->arena_len - o) cp = in->arena_len - o;
+      std::memcpy(s.h_arena + pos, in->arena + o, cp);
+      if (cp < len) std::memset(s.h_arena + pos + cp, 0, len - cp);  // past the arena
+      s.h_off[k] = pos;
+      s.h_len[k] = len;
+      s.h_ts[k] = in->ts_ns[f];
+      pos += len;
+    }
+  });
+  s.arena_used = part_bytes[parts];
+}
+
+int enqueue(tcbee_pipe* p, Slot& s, const tcbee_cfg* cfg) {
+  const uint64_t n = s.hi - s.lo, W = p->cfg.window;
+  // H2D
+  TRY_HIP(hipMemcpyAsync(s.d_arena, s.h_arena, s.arena_used, hipMemcpyHostToDevice, p->s_h2d));
+  if (!W) TRY_HIP(hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice, p->s_h2d));
+  TRY_HIP(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice, p->s_h2d));
+  TRY_HIP(hipMemcpyAsync(s.d_ts, s.h_ts, n * 8, hipMemcpyHostToDevice, p->s_h2d));
+  TRY_HIP(hipEventRecord(s.ev_h2d, p->s_h2d));
+  // parse (in chunk order on the context's stream: the flow table is shared)
+  TRY_HIP(hipStreamWaitEvent(p->s_comp, s.ev_h2d, 0));
+  if (W) {
+    const unsigned grid = unsigned(n / 256 + 1 < 4096 ? n / 256 + 1 : 4096);
+    hipLaunchKernelGGL(k_window_offsets, dim3(grid), dim3(256), 0, p->s_comp, s.d_off, n, W);
+    TRY_HIP(hipGetLastError());
+  }
+  TRY_HIP(hipMemsetAsync(s.d_meta, 0, 8 * sizeof(uint64_t), p->s_comp));
+  tcbee_frames din{s.d_arena, s.arena_used, s.d_off, s.d_len, s.d_ts, n};
+  const bool flows = !(cfg->flags & TCBEE_F_NO_FLOWS);
+  int rc = tcbee_parse_batch_device(p->ctx, &din, cfg, s.d_rec, n, nullptr,
+                                    flows ? s.d_id : nullptr, s.d_meta,
+                                    reinterpret_cast<tcbee_counters*>(s.d_meta + 1), p->s_comp);
+  if (rc) return rc;
+  TRY_HIP(hipMemcpyAsync(s.h_meta, s.d_meta, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                         p->s_comp));
+  TRY_HIP(hipEventRecord(s.ev_parse, p->s_comp));
+  return TCBEE_OK;
+}
+
+int fetch(tcbee_pipe* p, Slot& s, bool flows) {
+  TRY_HIP(hipEventSynchronize(s.ev_parse));
+  s.n_rec = s.h_meta[0];
+  if (s.n_rec) {
+    TRY_HIP(hipMemcpyAsync(s.h_rec, s.d_rec, s.n_rec * TCBEE_RECORD_BYTES, hipMemcpyDeviceToHost,
+                           p->s_d2h));
+    if (flows)
+      TRY_HIP(hipMemcpyAsync(s.h_id, s.d_id, s.n_rec * 4, hipMemcpyDeviceToHost, p->s_d2h));
+  }
+  TRY_HIP(hipEventRecord(s.ev_d2h, p->s_d2h));
+  return TCBEE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tcbee_pipe_create(tcbee_pipe** out, int device, const tcbee_pipe_cfg* pc,
+                      uint64_t max_flows) {
+  if (!out) return TCBEE_EINVAL;
+  *out = nullptr;
+  tcbee_pipe_cfg c = pc ? *pc : tcbee_pipe_cfg{};
+  if (!c.chunk_frames) c.chunk_frames = 1ull << 20;
+  if (!c.depth) c.depth = 3;
+  if (!c.threads) c.threads = 8;
+  if (c.depth < 3 || c.depth > 16 || c.threads > 256) return TCBEE_EINVAL;
+  if (c.window && (c.window < 80 || (c.window & 15u))) return TCBEE_EINVAL;
+  if (c.window) c.chunk_bytes = c.chunk_frames * c.window;
+  else if (!c.chunk_bytes) c.chunk_bytes = 512ull << 20;
+  tcbee_pipe* p = new (std::nothrow) tcbee_pipe;
+  if (!p) return TCBEE_ENOMEM;
+  p->device = device;
+  p->cfg = c;
+  int rc = tcbee_ctx_create(&p->ctx, device, c.chunk_frames, 0, max_flows ? max_flows : 1 << 20);
+  if (rc) return free_pipe(p), rc;
+  void* cs = nullptr;
+  tcbee_ctx_stream(p->ctx, &cs);
+  p->s_comp = static_cast<hipStream_t>(cs);
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&p->s_h2d, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&p->s_d2h, hipStreamNonBlocking) != hipSuccess)
+    return free_pipe(p), TCBEE_EDEVICE;
+  try {
+    p->slots.resize(c.depth);
+    p->pool = new Pool(c.threads);
+  } catch (...) {
+    return free_pipe(p), TCBEE_ENOMEM;
+  }
+  for (Slot& s : p->slots)
+    if ((rc = alloc_slot(p, s))) return free_pipe(p), rc;
+  *out = p;
+  return TCBEE_OK;
+}
+
+int tcbee_pipe_destroy(tcbee_pipe* p) {
+  if (!p) return TCBEE_EINVAL;
+  free_pipe(p);
+  return TCBEE_OK;
+}
+
+int tcbee_pipe_ctx(tcbee_pipe* p, tcbee_ctx** ctx) {
+  if (!p || !ctx) return TCBEE_EINVAL;
+  *ctx = p->ctx;
+  return TCBEE_OK;
+}
+
+int tcbee_pipe_get_stats(const tcbee_pipe* p, tcbee_pipe_stats* st) {
+  if (!p || !st) return TCBEE_EINVAL;
+  *st = p->st;
+  return TCBEE_OK;
+}
+
+int tcbee_pipe_run(tcbee_pipe* p, const tcbee_frames* in, const tcbee_cfg* cfg,
+                   uint8_t* out_rec74, uint64_t out_cap, uint32_t* out_flow_id,
+                   tcbee_pipe_sink_fn fn, void* user, uint64_t* out_n, tcbee_counters* ctr) {
+  if (!p || !in || !cfg || !out_n) return TCBEE_EINVAL;
+  if (in->n && (!in->arena || !in->offset || !in->caplen || !in->ts_ns)) return TCBEE_EINVAL;
+  if (out_cap && !out_rec74) return TCBEE_EINVAL;
+  if (!p->cfg.window)
+    for (uint64_t i = 0; i < in->n; ++i)
+      if (in->caplen[i] > p->cfg.chunk_bytes) return TCBEE_ECAPACITY;
+  TRY_HIP(hipSetDevice(p->device));
+  const bool flows = !(cfg->flags & TCBEE_F_NO_FLOWS);
+  const uint64_t D = p->slots.size();
+  uint64_t written = 0, records = 0, chunks = 0;
+  tcbee_counters sum{};
+  int rc = TCBEE_OK;
+
+  auto consume = [&](Slot& s) -> int {
+    TRY_HIP(hipEventSynchronize(s.ev_d2h));
+    sum.ingress += s.h_meta[1];
+    sum.egress += s.h_meta[2];
+    sum.handled += s.h_meta[3];
+    sum.dropped += s.h_meta[4];
+    const uint64_t n = s.n_rec;
+    s.first_record = records;
+    if (out_rec74 && records < out_cap) {
+      const uint64_t k = n < out_cap - records ? n : out_cap - records;
+      uint8_t* dst = out_rec74 + records * TCBEE_RECORD_BYTES;
+      uint32_t* did = out_flow_id ? out_flow_id + records : nullptr;
+      p->pool->run([&](unsigned part, unsigned parts) {
+        const uint64_t a = k * part / parts, b = k * (part + 1) / parts;
+        std::memcpy(dst + a * TCBEE_RECORD_BYTES, s.h_rec + a * TCBEE_RECORD_BYTES,
+                    (b - a) * TCBEE_RECORD_BYTES);
+        if (did && flows) std::memcpy(did + a, s.h_id + a, (b - a) * 4);
+      });
+      written += k;
+    }
+    records += n;
+    if (fn) {
+      int urc = fn(user, s.h_rec, flows ? s.h_id : nullptr, n, s.first_record);
+      if (urc) return urc;
+    }
+    return TCBEE_OK;
+  };
+
+  // Chunk c lives in slot c % D. Steady state at the top of an iteration:
+  // issued = i, fetched = i-1, consumed = i-2 — stage(i) overlaps H2D/parse of
+  // i-1 and the D2H of i-2 already in flight.
+  uint64_t lo = 0, issued = 0, fetched = 0, consumed = 0;
+  while (rc == TCBEE_OK && (lo < in->n || consumed < issued)) {
+    if (lo < in->n) {
+      while (rc == TCBEE_OK && consumed + D <= issued) {  // slot reuse
+        if (fetched <= consumed) rc = fetch(p, p->slots[fetched++ % D], flows);
+        if (rc == TCBEE_OK) rc = consume(p->slots[consumed++ % D]);
+      }
+      if (rc) break;
+      Slot& s = p->slots[issued % D];
+      s.lo = lo;
+      s.hi = chunk_end(p, in, lo);
+      stage(p, in, s);
+      if ((rc = enqueue(p, s, cfg))) break;
+      lo = s.hi;
+      ++issued;
+      ++chunks;
+    }
+    const bool tail = lo >= in->n;
+    if (fetched + 1 < issued || (tail && fetched < issued))
+      rc = fetch(p, p->slots[fetched++ % D], flows);
+    if (rc == TCBEE_OK && (consumed + 1 < fetched || (tail && consumed < fetched)))
+      rc = consume(p->slots[consumed++ % D]);
+  }
+  (void)hipStreamSynchronize(p->s_h2d);
+  (void)hipStreamSynchronize(p->s_d2h);
+  (void)tcbee_ctx_sync(p->ctx);
+  if (rc) return rc;
+  *out_n = records;
+  p->st.frames += in->n;
+  p->st.records += records;
+  p->st.chunks += chunks;
+  if (ctr) {
+    ctr->ingress += sum.ingress;
+    ctr->egress += sum.egress;
+    ctr->handled += sum.handled;
+    ctr->dropped += sum.dropped;
+  }
+  // records beyond out_cap were produced and handed to fn but not copied
+  if (out_rec74 && records > out_cap) return TCBEE_ECAPACITY;
+  return tcbee_ctx_status(p->ctx);
+}
+
+}  // extern "C"

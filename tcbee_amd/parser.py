@@ -59,15 +59,26 @@ class PacketParser:
                                       C.c_uint64(max_arena), C.c_uint64(max_flows)),
                    "tcbee_ctx_create")
         self._h = h
+        self._owned = True
         self.device = device
         self.max_frames = max_frames
         self.max_arena = max_arena
         self.max_flows = max_flows
 
+    @classmethod
+    def _borrow(cls, handle: C.c_void_p, device: int, max_frames: int, max_flows: int):
+        """A non-owning view of a context owned elsewhere (e.g. an ingest pipeline)."""
+        self = cls.__new__(cls)
+        self._h, self._owned = handle, False
+        self.device, self.max_frames, self.max_arena, self.max_flows = (device, max_frames, 0,
+                                                                        max_flows)
+        return self
+
     # -- lifetime -----------------------------------------------------------
     def close(self) -> None:
         if self._h:
-            _lib.lib().tcbee_ctx_destroy(self._h)
+            if self._owned:
+                _lib.lib().tcbee_ctx_destroy(self._h)
             self._h = None
 
     def __enter__(self):

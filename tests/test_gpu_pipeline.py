@@ -1,0 +1,135 @@
+"""GPU: the host-frames ingest pipeline (tcbee_pipe) and the end-to-end pcap
+replay. Every output is compared with the CPU oracle fed the same frames."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import tcbee_amd
+from tcbee_amd import host
+from tcbee_amd.pipeline import Pipeline, replay_pcap
+from tracegen import mixed_trace
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import process_ref  # noqa: E402  (test infrastructure only)
+
+pytestmark = pytest.mark.gpu
+
+
+def check_same(res, orc, flows_gpu=None):
+    rec, fh, fi, ctr, table = orc
+    assert res.n == len(rec)
+    assert np.array_equal(res.records, rec)
+    if res.flow_id is not None:
+        assert np.array_equal(res.flow_id, fi)
+    assert res.counters == ctr
+    if flows_gpu is not None:
+        assert np.array_equal(flows_gpu, table)
+
+
+@pytest.mark.parametrize("window,chunk,depth,threads", [
+    (80, 4096, 3, 8), (80, 1000, 4, 1), (0, 4096, 3, 8), (96, 65536, 5, 3), (0, 777, 3, 2),
+])
+def test_pipeline_matches_oracle(gpu, oracle, window, chunk, depth, threads):
+    t = mixed_trace(60_000, seed=100 + chunk, n_flows=300)
+    with Pipeline(device=0, chunk_frames=chunk, window=window, depth=depth,
+                  threads=threads, max_flows=1 << 12) as p:
+        res = p.run(t)
+        check_same(res, oracle.parse(t), p.flows())
+        st = p.stats()
+        assert st["frames"] == t.n and st["chunks"] >= t.n // chunk
+
+
+def test_pipeline_whole_frames_byte_budget(gpu, oracle):
+    """window 0 with a tiny chunk_bytes: chunks are cut by bytes, not frames."""
+    t = mixed_trace(20_000, seed=7)
+    with Pipeline(device=0, chunk_frames=1 << 16, window=0, chunk_bytes=64 * 1024) as p:
+        res = p.run(t)
+        check_same(res, oracle.parse(t), p.flows())
+        assert p.stats()["chunks"] > 20
+
+
+def test_pipeline_filter_egress_noflows(gpu, oracle):
+    t = mixed_trace(30_000, seed=8)
+    with Pipeline(device=0, chunk_frames=5000) as p:
+        res = p.run(t, filter_port=5201, direction=tcbee_amd.DIR_EGRESS)
+        check_same(res, oracle.parse(t, filter_port=5201, direction=1))
+        res2 = p.run(t, flows=False)
+        rec, _, _, ctr, _ = oracle.parse(t, flows=False)
+        assert np.array_equal(res2.records, rec) and res2.counters == ctr
+        assert res2.flow_id is None
+
+
+def test_pipeline_calls_continue_flow_ids(gpu, oracle):
+    """Two runs on one pipe = one trace: ids continue, like tcbee_parse_batch."""
+    t = mixed_trace(40_000, seed=9, n_flows=500)
+    a, b = t.slice(0, 17_000), t.slice(17_000, t.n)
+    with Pipeline(device=0, chunk_frames=4096) as p:
+        ra = p.run(a)
+        rb = p.run(b)
+        ft = oracle.new_flowtab(4096)
+        oa = oracle.parse(a, ft=ft)
+        ob = oracle.parse(b, ft=ft, record_base=len(oa[0]))
+        table = oracle.flows(ft)
+        oracle.free_flowtab(ft)
+        assert np.array_equal(ra.flow_id, oa[2]) and np.array_equal(rb.flow_id, ob[2])
+        assert np.array_equal(p.flows(), table)
+
+
+def test_pipeline_sink_callback_and_out_cap(gpu, oracle):
+    t = mixed_trace(25_000, seed=10)
+    rec, fh, fi, ctr, _ = oracle.parse(t)
+    got, ids, firsts = [], [], []
+    with Pipeline(device=0, chunk_frames=3000) as p:
+        res = p.run(t, collect=False,
+                    sink=lambda r, i, first: (got.append(r.copy()), ids.append(i.copy()),
+                                              firsts.append(first)))
+        assert res.n == len(rec) and res.records is None
+        assert np.array_equal(np.concatenate(got), rec)
+        assert np.array_equal(np.concatenate(ids), fi)
+        assert firsts == list(np.cumsum([0] + [len(g) for g in got[:-1]]))
+        small = np.empty((100, 74), np.uint8)
+        p.reset_flows()
+        with pytest.raises(tcbee_amd.TcbeeError) as e:
+            p.run(t, out_rec=small, out_id=np.empty(100, np.uint32))
+        assert e.value.code == tcbee_amd._lib.ECAPACITY
+        assert np.array_equal(small, rec[:100])
+
+
+def test_pipeline_empty_and_tiny(gpu, oracle):
+    with Pipeline(device=0, chunk_frames=1024) as p:
+        t0 = mixed_trace(0, seed=1)
+        r0 = p.run(t0)
+        assert r0.n == 0
+        t1 = mixed_trace(5, seed=1)
+        check_same(p.run(t1), oracle.parse(t1))
+
+
+def test_replay_pcap_end_to_end(gpu, oracle, tmp_path):
+    """pcap -> GPU -> xdp.tcp + SQLite + metrics.json, each equal to the oracle path."""
+    t = mixed_trace(30_000, seed=77, n_flows=40)
+    # unique timestamps per flow keep the database out of the duplicate-timestamp wedge
+    pcap = str(tmp_path / "trace.pcap")
+    host.write_pcap(pcap, t)
+    prefix = str(tmp_path) + "/run_"
+    out = replay_pcap(pcap, prefix, db_path=str(tmp_path / "gpu.sqlite"), chunk_frames=4096)
+    rec, fh, fi, ctr, table = oracle.parse(t)
+    assert out["records"] == len(rec) and out["counters"] == ctr and out["flows"] == len(table)
+    data = open(prefix + "xdp.tcp", "rb").read()
+    assert data == rec.tobytes()
+    process_ref.process_records(rec.tobytes(), str(tmp_path / "orc.sqlite"))
+    assert process_ref.dump_db(str(tmp_path / "gpu.sqlite")) == \
+        process_ref.dump_db(str(tmp_path / "orc.sqlite"))
+    m = json.load(open(prefix + "metrics.json"))
+    assert m == {"handled": ctr["handled"], "dropped": ctr["dropped"],
+                 "ingress": ctr["ingress"], "egress": ctr["egress"],
+                 "ingress_calls": 0, "egress_calls": 0}
+    # the tcbee-process stage over the written file gives the same database again
+    host.process_files(prefix, str(tmp_path / "proc.sqlite"))
+    assert process_ref.dump_db(str(tmp_path / "proc.sqlite")) == \
+        process_ref.dump_db(str(tmp_path / "orc.sqlite"))
