@@ -158,20 +158,66 @@ def cpu_baseline(sizes, kind, n_flows, seed, seconds, threads, sample_n=2_000_00
     return out, tr.n
 
 
-def host_path_e2e(sizes, kind, n_flows, seed, n=4_000_000, reps=3):
-    """End-to-end rate through the host-pointer entry point: pageable H2D of the frames,
-    parse, D2H of records + flow hash/id (tcbee_parse_batch)."""
+def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=5, threads=16):
+    """End-to-end rates from host memory: frames in pageable host RAM -> records +
+    flow ids back in pageable host RAM (H2D and D2H inside the timed region).
+      pipe_window80: tcbee_pipe, header-window staging (80 B/frame shipped)
+      pipe_whole:    tcbee_pipe, whole frames shipped
+      parse_batch:   one synchronous tcbee_parse_batch call (no overlap), 4M frames"""
+    import numpy as np
+
     import tcbee_amd
+    from tcbee_amd.pipeline import Pipeline
     tr = tcbee_amd.synth_trace(n, sizes=sizes, kind=kind, n_flows=n_flows, seed=seed)
-    with tcbee_amd.PacketParser(max_frames=n, max_arena=len(tr.arena),
+    rec = np.empty((n, 74), np.uint8)
+    ids = np.empty(n, np.uint32)
+    out = {"frames": n, "threads": threads, "arena_bytes": int(len(tr.arena))}
+    for name, window in (("pipe_window80", 80), ("pipe_whole", 0)):
+        with Pipeline(device=0, chunk_frames=1 << 20, window=window, depth=4, threads=threads,
+                      chunk_bytes=(1 << 29), max_flows=max(4 * n_flows, 1 << 12)) as p:
+            p.run(tr, out_rec=rec, out_id=ids)
+            ts = []
+            for _ in range(reps):
+                p.reset_flows()
+                t0 = time.perf_counter()
+                r = p.run(tr, out_rec=rec, out_id=ids)
+                ts.append(time.perf_counter() - t0)
+            el = float(np.median(ts))
+        h2d = n * (window + 12) if window else int(len(tr.arena)) + 20 * n
+        out[name] = {"mpkts": round(n / el / 1e6, 1), "s": round(el, 4), "records": r.n,
+                     "h2d_bytes": h2d, "h2d_GBs": round(h2d / el / 1e9, 1)}
+    m = 4_000_000
+    sub = tr.slice(0, m)
+    with tcbee_amd.PacketParser(max_frames=m, max_arena=len(sub.arena),
                                 max_flows=max(4 * n_flows, 1 << 12)) as p:
-        p.parse(tr)
+        p.parse(sub)
         t0 = time.perf_counter()
-        for _ in range(reps):
-            r = p.parse(tr)
-        el = (time.perf_counter() - t0) / reps
-    return {"mpkts": n / el / 1e6, "frames": n, "bytes_h2d": int(len(tr.arena)) + 20 * n,
-            "records": r.n}
+        for _ in range(3):
+            p.reset_flows()
+            r = p.parse(sub)
+        el = (time.perf_counter() - t0) / 3
+    out["parse_batch"] = {"mpkts": round(m / el / 1e6, 1), "frames": m}
+    return out
+
+
+def pmc_traffic(args, k1_ms):
+    """roofline.traffic: HBM bytes per k_parse launch from the committed rocprofv3 PMC
+    passes of this same command (profiles/pmc_k_parse.json, written by
+    tools/prof_summary.py: 2 x FETCH_SIZE + WRITE_SIZE). PMC counters cannot be
+    read from inside the timed run, so they come from the separate --pmc runs;
+    null when the committed profile is for another workload."""
+    path = os.path.join(ROOT, "profiles", "pmc_k_parse.json")
+    try:
+        pmc = json.load(open(path))
+    except (OSError, ValueError):
+        return {"traffic": None}
+    if (pmc.get("frames") != args.frames or pmc.get("sizes") != args.sizes
+            or pmc.get("flows") != args.flows):
+        return {"traffic": None}
+    t = float(pmc["traffic_bytes_per_launch"])
+    return {"traffic": round(t / 1e9, 3), "traffic_unit": "GB/launch (HBM, PMC)",
+            "traffic_per_frame": round(t / args.frames, 1),
+            "traffic_GBs": round(t / (k1_ms * 1e-3) / 1e9, 1)}
 
 
 def main():
@@ -186,6 +232,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip config-2 and e2e legs")
+    ap.add_argument("--e2e-frames", type=int, default=20_000_000)
     args = ap.parse_args()
 
     import torch
@@ -237,7 +284,7 @@ def main():
                        "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel": "k_parse",
+                         **pmc_traffic(args, k1_ms), "kernel": "k_parse",
                          "k1_ms": round(k1_ms, 4),
                          "alg_bytes_per_frame": IDX_BYTES + hdr + OUT_BYTES},
             "check": check,
@@ -248,7 +295,8 @@ def main():
             out["config2_1M_64B"] = {"mpkts": round(1_000_000 * max(args.steps, 20) / e_el / 1e6, 1),
                                      "ms_per_step": round(e_el / max(args.steps, 20) * 1e3, 4),
                                      "k1_ms": round(e_k1, 4), "check": e_chk}
-            out["e2e_host_path"] = host_path_e2e(args.sizes, kind, args.flows, args.seed)
+            out["e2e_host"] = host_e2e(args.sizes, kind, args.flows, args.seed,
+                                       n=args.e2e_frames)
         if not args.no_cpu and world == 1:
             threads = min(16, os.cpu_count() or 1)
             res, sample_n = cpu_baseline(args.sizes, kind, args.flows, args.seed,

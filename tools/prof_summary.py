@@ -52,6 +52,7 @@ def main():
         write = statistics.median(wk) * 1024
         traffic = fetch + write
         pmc = {"kernel": "k_parse", "workload": "config3 100M IMIX 10k flows",
+               "frames": 100_000_000, "sizes": "imix", "flows": 10_000,
                "fetch_bytes_corrected": fetch, "write_bytes": write,
                "traffic_bytes_per_launch": traffic, "fetch_size_kib_raw": statistics.median(fk),
                "write_size_kib_raw": statistics.median(wk), "dispatches": len(fk),
