@@ -21,6 +21,9 @@ struct tcbee_ctx {
   int fpl = 2;
   bool reset_pending = false;   // tcbee_flow_reset_device: applied by the next launch
   uint32_t withhold_every = 0;  // TCBEE_TEST_WITHHOLD (look-back recount test hook)
+  uint64_t k3_pk_budget = 0;    // TCBEE_TEST_K3_BUDGET (K3 wave-flush test hook)
+  int k3_atomic_flush = 0;      // TCBEE_K3_ATOMIC=1: K3 flushes bins with device atomics (A/B)
+  int k3_meta_gather = 0;       // TCBEE_K3_META=1: K3 gathers ids from the 64-B entries (A/B)
 
   FlowTable tab{};
   uint64_t nslots = 0;
@@ -34,6 +37,7 @@ struct tcbee_ctx {
   uint32_t* d_bprefix = nullptr;
   uint32_t* d_slot_scratch = nullptr;
   uint32_t* d_len_scratch = nullptr;
+  uint64_t* d_count_part = nullptr;  // K3 per-block partial bins [n_cu][kCountBins]
   int n_cu = 256;
   uint64_t max_words = 0, max_sblocks = 0;
 
@@ -143,6 +147,7 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   dfree(c->tab.meta);
   dfree(c->tab.cnt);
+  dfree(c->tab.sid);
   dfree(c->d_persist);
   dfree(c->d_batch);
   dfree(c->d_tile_status);
@@ -152,6 +157,7 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
   dfree(c->d_bprefix);
   dfree(c->d_slot_scratch);
   dfree(c->d_len_scratch);
+  dfree(c->d_count_part);
   dfree(c->d_arena);
   dfree(c->d_off);
   dfree(c->d_len);
@@ -185,6 +191,9 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   c->max_arena = max_arena;
   c->max_flows = max_flows < 16 ? 16 : max_flows;
   if (const char* e = std::getenv("TCBEE_TEST_WITHHOLD")) c->withhold_every = (uint32_t)std::atoi(e);
+  if (const char* e = std::getenv("TCBEE_TEST_K3_BUDGET")) c->k3_pk_budget = std::strtoull(e, nullptr, 10);
+  if (const char* e = std::getenv("TCBEE_K3_ATOMIC")) c->k3_atomic_flush = std::atoi(e);
+  if (const char* e = std::getenv("TCBEE_K3_META")) c->k3_meta_gather = std::atoi(e);
   if (const char* e = std::getenv("TCBEE_FPL")) {
     const int v = std::atoi(e);
     if (v == 1 || v == 2 || v == 4) c->fpl = v;
@@ -206,6 +215,7 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   hipError_t e = hipSuccess;
   if ((e = dalloc(&c->tab.meta, 8 * c->nslots)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.cnt, 2 * c->nslots)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->tab.sid, c->nslots)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_persist, 1)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_batch, 1)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_tile_status, c->max_tiles)) != hipSuccess) return fail(map_err(e));
@@ -218,6 +228,9 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->n_cu = prop.multiProcessorCount;
+  // K3's grid is at most n_cu blocks (launch site), one partial-bin row each
+  if ((e = dalloc(&c->d_count_part, (uint64_t)c->n_cu * kCountBins)) != hipSuccess)
+    return fail(map_err(e));
   rc = tcbee_flow_reset(c);
   if (rc != TCBEE_OK) return fail(rc);
   *out = c;
@@ -347,7 +360,11 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     k.batch = c->d_batch;
     k.persist = c->d_persist;
     k.meta = c->tab.meta;
+    k.sid = c->k3_meta_gather ? nullptr : c->tab.sid;
     k.cnt = c->tab.cnt;
+    k.part = c->k3_atomic_flush ? nullptr : c->d_count_part;
+    k.wave_pk_budget = c->k3_pk_budget && c->k3_pk_budget < kWavePkBudget ? c->k3_pk_budget
+                                                                           : kWavePkBudget;
     // trade-off: more blocks = more latency hidden; each block flushes every bin it
     // touched, so a block should see a few thousand records
     const uint64_t want = (in->n + 8191) / 8192;

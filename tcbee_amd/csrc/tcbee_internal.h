@@ -21,6 +21,8 @@ struct FlowTable {
   uint64_t* meta;
   uint64_t* cnt;
   uint64_t mask;  // slots - 1
+  uint32_t* sid;  // slot -> dense id (0-based), valid once meta[7] != 0; K3's compact
+                  // gather source (4 B per slot instead of a 64-B entry)
 };
 
 // Lives across batches of one context.
@@ -103,7 +105,11 @@ struct CountArgs {
   const BatchState* batch;
   const PersistState* persist;
   const uint64_t* meta;
+  const uint32_t* sid;       // nullptr: gather ids from meta (A/B, TCBEE_K3_META=1)
   uint64_t* cnt;
+  uint64_t wave_pk_budget;   // records a wave adds to the LDS bins between its flushes
+  uint64_t* part;            // [gridDim.x][kCountBins] per-block packed bins (LDS path);
+                             // nullptr: flush the bins with device atomics instead
 };
 hipError_t launch_count(const CountArgs& c, unsigned grid, hipStream_t s);
 
@@ -134,6 +140,9 @@ constexpr int kBlock = 256;
 constexpr int kScanWordsPerBlock = 2048;  // 256 threads x 8 words
 constexpr uint64_t kRankSmallWords = 1024 * 32;  // single-block rank up to 1M frames
 constexpr int kCountBlock = 1024;
-constexpr int kCountBins = 16384;         // 2 x 64 KiB of LDS
+constexpr int kCountBins = 16384;         // 128 KiB of LDS (u64 bins)
+constexpr int kBinPkShift = 40;           // K3 bin: pkts in bits 63:40, bytes in 39:0
+constexpr uint64_t kWavePkBudget = (1ull << (64 - kBinPkShift)) / (kCountBlock / 64);  // 2^20
+constexpr uint64_t kWaveByBudget = (1ull << kBinPkShift) / (kCountBlock / 64);         // 2^36
 
 }  // namespace tcbee

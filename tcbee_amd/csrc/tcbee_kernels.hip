@@ -129,12 +129,19 @@ __device__ __forceinline__ void load_windows(const uint8_t* __restrict__ arena, 
 #pragma unroll
   for (int f = 0; f < FPL; ++f) put_chunk(w[f], 5, make_uint4(0u, 0u, 0u, 0u));
   if (__all(inb)) {
+    // Only the chunks holding frame bytes [12, 52) — ethertype .. TCP checksum,
+    // all an IPv4 record uses (the MACs and the urgent pointer are never read):
+    // 3 or 4 chunks instead of 5, so a window touches one 64-B sector more
+    // often. Lanes whose chunk is not needed are masked off the load.
 #pragma unroll
     for (int f = 0; f < FPL; ++f) {
       const u32x4* src = reinterpret_cast<const u32x4*>(arena + (off[f] & ~15ull));
+      const uint32_t sh = (uint32_t)(off[f] & 15u);
+      const uint32_t c_lo = (sh + kFirstUsedByte) >> 4, c_hi = (sh + kV4LastUsedByte) >> 4;
 #pragma unroll
       for (int c = 0; c < 5; ++c) {
-        const u32x4 v = ld_stream<NT>(src + c);
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if ((uint32_t)c >= c_lo && (uint32_t)c <= c_hi) v = ld_stream<NT>(src + c);
         put_chunk(w[f], c, make_uint4(v[0], v[1], v[2], v[3]));
       }
     }
@@ -161,7 +168,6 @@ __device__ __forceinline__ bool parse_window(const uint8_t* __restrict__ arena, 
   if (caplen < kEthHdrLen) return false;  // xdp.rs:37-39
   const uint64_t abase = off & ~15ull;
   const uint32_t s = NOLOAD ? 0u : (uint32_t)(off & 15u);
-  const uint32_t need4 = s + (caplen < kV4MinLen ? caplen : kV4MinLen);
   if (!NOLOAD) {
     // ethertype straight from the raw window: bytes s+12, s+13 (dwords 3..7)
     const uint32_t e = s + 12, t3 = (e >> 2) - 3, m1 = 0u - (t3 & 1u), m2 = 0u - ((t3 >> 1) & 1u);
@@ -169,13 +175,13 @@ __device__ __forceinline__ bool parse_window(const uint8_t* __restrict__ arena, 
     const uint32_t x2 = (w[5] & ~m1) | (w[6] & m1), x3 = (w[6] & ~m1) | (w[7] & m1);
     const uint32_t lo = (x0 & ~m2) | (x2 & m2), hi = (x1 & ~m2) | (x3 & m2);
     const uint32_t et = bswap16(align_bytes(hi, lo, e & 3u) & 0xFFFFu);
-    const uint32_t need6 = s + (caplen < kV6MinLen ? caplen : kV6MinLen);
-    if (et == kEthertypeIPv6 && need6 > need4) {
-      // IPv6 tail: chunks of [need4, need6) not loaded yet (chunk 5, or 3..5 on
-      // the bounds-checked path, where chunks past need4 were left zero)
+    const uint32_t need6 = s + (caplen < kV6LastUsedByte + 1 ? caplen : kV6LastUsedByte + 1);
+    if (et == kEthertypeIPv6) {
+      // IPv6 tail: the chunks holding frame bytes [52, 72) (TCP header at 54),
+      // which the IPv4 window never loads
 #pragma unroll
       for (int c = 3; c < 6; ++c) {
-        if ((uint32_t)(16 * c) < need6 && ((uint32_t)(16 * c) >= need4 || c == 5))
+        if ((uint32_t)(16 * c) < need6 && (uint32_t)(16 * c + 16) > s + kV4LastUsedByte + 1)
           put_chunk(w, c, load_chunk(arena, arena_len, abase + 16u * c));
       }
     }
@@ -765,46 +771,84 @@ __global__ void k_prep(PrepArgs p) {
 // ---------------------------------------------------------------------------
 // K2: ranks of this batch's new flows by first_seen
 // ---------------------------------------------------------------------------
-// Small batches (nwords <= kRankSmallWords): mark + scan + assign in ONE block.
+// Small batches (nwords <= kRankSmallWords): rank in ONE block.
+//  - n_new <= kRankSortMax: rank = number of this batch's new flows seen earlier,
+//    counted over the first_seen values staged in LDS (no bitmap pass at all);
+//  - otherwise mark + scan + assign: the bitmap is scanned by 16 waves, each over
+//    a contiguous word range read 64 consecutive words at a time (coalesced).
+constexpr uint32_t kRankSortMax = 2048;
+
 __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
+  __shared__ uint32_t s_fs[kRankSortMax];
   __shared__ uint32_t s_tmp[16];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint64_t n_new = r.batch->n_new;
   const uint64_t base = r.persist->rec_base;
   const uint64_t fbase = r.persist->flow_count;
+  if (tid == 0) r.batch->flow_total = fbase + n_new;
+  if (n_new <= kRankSortMax) {
+    for (uint32_t j = tid; j < n_new; j += 1024)
+      s_fs[j] = (uint32_t)(r.tab.meta[8 * r.new_list[j] + 6] - base);
+    for (uint32_t j = (uint32_t)n_new + tid; j < ((uint32_t)n_new + 3u) / 4u * 4u; j += 1024)
+      s_fs[j] = 0xFFFFFFFFu;  // pad to a multiple of 4 (never below a real value)
+    __syncthreads();
+    const uint32_t n4 = ((uint32_t)n_new + 3u) / 4u;
+    const uint4* v4 = reinterpret_cast<const uint4*>(s_fs);
+    for (uint32_t j = tid; j < n_new; j += 1024) {
+      const uint32_t v = s_fs[j];
+      uint32_t rank = 0;
+      for (uint32_t i = 0; i < n4; ++i) {  // broadcast reads: every lane reads the same word
+        const uint4 q = v4[i];
+        rank += (q.x < v) + (q.y < v) + (q.z < v) + (q.w < v);
+      }
+      const uint64_t sl = r.new_list[j];
+      r.tab.meta[8 * sl + 7] = fbase + rank + 1;
+      r.tab.sid[sl] = (uint32_t)(fbase + rank);
+    }
+    return;
+  }
   for (uint64_t j = tid; j < n_new; j += 1024) {
     const uint64_t local = r.tab.meta[8 * r.new_list[j] + 6] - base;
     if ((local >> 5) < r.nwords) atomicOr(&r.bitmap[local >> 5], 1u << (local & 31));
   }
   __syncthreads();
-  // exclusive popcount prefix per word: thread t owns words [t*wpt, (t+1)*wpt),
-  // wpt <= 64, all loaded into registers at once (independent loads in flight)
-  constexpr int kMaxWpt = (int)(kRankSmallWords / 1024);
-  const uint32_t wpt = (uint32_t)((r.nwords + 1023) / 1024);
-  const uint64_t w0 = (uint64_t)tid * wpt;
-  uint32_t wv[kMaxWpt];
+  // wave w owns words [w*per, (w+1)*per), per a multiple of 64; lane l holds words
+  // w*per + 64k + l in wv[k]. Wave totals first (for the wave's base), then a
+  // per-64-word scan writes the exclusive prefixes.
+  constexpr int kMaxK = (int)(kRankSmallWords / 1024);
+  const uint32_t per = (uint32_t)((r.nwords + 16 * 64 - 1) / (16 * 64)) * 64u;
+  const uint64_t w0 = (uint64_t)wave * per;
+  const uint32_t kk = per / 64u;
+  uint32_t wv[kMaxK];
+  uint32_t mine = 0;
 #pragma unroll
-  for (int k = 0; k < kMaxWpt; ++k)
-    wv[k] = ((uint32_t)k < wpt && w0 + k < r.nwords)
-                ? __hip_atomic_load(&r.bitmap[w0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+  for (int k = 0; k < kMaxK; ++k) {
+    const uint64_t w = w0 + 64u * k + lane;
+    wv[k] = ((uint32_t)k < kk && w < r.nwords)
+                ? __hip_atomic_load(&r.bitmap[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                 : 0u;
-  uint32_t sum = 0;
-#pragma unroll
-  for (int k = 0; k < kMaxWpt; ++k) sum += __popc(wv[k]);
-  uint32_t x = sum;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o);
-    if (lane >= (uint32_t)o) x += y;
+    mine += __popc(wv[k]);
   }
-  if (lane == 63) s_tmp[wave] = x;
-  __syncthreads();
-  uint32_t pre = x - sum;
-  for (uint32_t w = 0; w < wave; ++w) pre += s_tmp[w];
 #pragma unroll
-  for (int k = 0; k < kMaxWpt; ++k) {
-    if ((uint32_t)k < wpt && w0 + k < r.nwords) r.wprefix[w0 + k] = pre;
-    pre += __popc(wv[k]);
+  for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o);
+  if (lane == 0) s_tmp[wave] = mine;
+  __syncthreads();
+  uint32_t carry = 0;
+  for (uint32_t w = 0; w < wave; ++w) carry += s_tmp[w];
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k) {
+    if ((uint32_t)k < kk) {  // wave-uniform
+      const uint32_t c = __popc(wv[k]);
+      uint32_t x = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= (uint32_t)o) x += y;
+      }
+      const uint64_t w = w0 + 64u * k + lane;
+      if (w < r.nwords) r.wprefix[w] = carry + x - c;
+      carry += __shfl(x, 63);
+    }
   }
   __syncthreads();
   for (uint64_t j = tid; j < n_new; j += 1024) {
@@ -814,8 +858,8 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
     const uint32_t below = __hip_atomic_load(&r.bitmap[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
                            ((1u << (local & 31)) - 1u);
     r.tab.meta[8 * s + 7] = fbase + r.wprefix[w] + __popc(below) + 1;
+    r.tab.sid[s] = (uint32_t)(fbase + r.wprefix[w] + __popc(below));
   }
-  if (tid == 0) r.batch->flow_total = fbase + n_new;
 }
 
 __global__ void k_mark(RankArgs r) {
@@ -895,21 +939,29 @@ __global__ void k_assign(RankArgs r) {
     const uint32_t below = r.bitmap[w] & ((1u << (local & 31)) - 1u);
     const uint64_t id = fbase + r.bprefix[w / kScanWordsPerBlock] + r.wprefix[w] + __popc(below);
     r.tab.meta[8 * s + 7] = id + 1;
+    r.tab.sid[s] = (uint32_t)id;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) r.batch->flow_total = fbase + n_new;
 }
 
 // K3: per accepted frame, slot -> dense id (written for records p < out_cap) and
 // pkts/bytes per flow. While every flow fits the LDS bins (<= kCountBins), each
-// block histograms a contiguous range of accepted frames in LDS and flushes the
-// non-zero bins with one global atomic pair each; bins are u32 and a block
-// flushes before its running byte total could wrap one. Otherwise per-frame
-// global atomics (wave-uniform flows aggregated first).
+// block histograms a contiguous range of accepted frames in LDS — one 64-bit
+// bin per flow, pkts in bits 63:40 and bytes in bits 39:0, one LDS atomic per
+// record (one per wave when the wave's records share a flow) — and flushes the
+// non-zero bins with one global atomic pair each at the end. No block barrier
+// inside the loop: each wave tracks what it added since its last flush and,
+// before its share could overflow a bin field, flushes every bin itself with
+// atomic exchanges (exact under concurrent adds; never taken at realistic
+// sizes). Frames longer than 2^24 bytes go straight to global atomics.
+// With more flows than bins: per-frame global atomics (wave-uniform flows
+// aggregated first).
+constexpr uint64_t kBinByMask = (1ull << kBinPkShift) - 1;
+constexpr uint32_t kBigLen = 1u << 24;
+
 __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
-  __shared__ uint32_t s_pk[kCountBins];
-  __shared__ uint32_t s_by[kCountBins];
-  __shared__ uint64_t s_red[kCountBlock / 64];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  __shared__ uint64_t s_bin[kCountBins];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint64_t n_acc = c.batch->n_acc;
   const uint64_t nflows = c.batch->flow_total;
   if (blockIdx.x == 0 && tid == 0) {
@@ -925,64 +977,66 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
     c.persist_rw->rec_base += n_acc;
     c.persist_rw->flow_count = nflows;
   }
+  constexpr int U = 8;  // records per thread per iteration (loads issued together)
   const bool use_lds = nflows <= (uint64_t)kCountBins;
-  const uint64_t per = ((n_acc + gridDim.x - 1) / gridDim.x + 4 * kCountBlock - 1) / (4 * kCountBlock) * (4 * kCountBlock);
+  const uint64_t per = ((n_acc + gridDim.x - 1) / gridDim.x + U * kCountBlock - 1) /
+                       (U * kCountBlock) * (U * kCountBlock);
   const uint64_t lo = (uint64_t)blockIdx.x * per;
   const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
   if (use_lds) {
-    for (uint32_t b = tid; b < nflows; b += kCountBlock) s_pk[b] = s_by[b] = 0;
+    for (uint32_t b = tid; b < nflows; b += kCountBlock) s_bin[b] = 0;
     __syncthreads();
   }
-  auto flush = [&]() {
-    __syncthreads();
-    for (uint32_t b = tid; b < nflows; b += kCountBlock) {
-      const uint32_t pk = s_pk[b];
-      if (pk) {
-        atomicAdd((unsigned long long*)&c.cnt[2ull * b], (unsigned long long)pk);
-        atomicAdd((unsigned long long*)&c.cnt[2ull * b + 1], (unsigned long long)s_by[b]);
-        s_pk[b] = 0;
-        s_by[b] = 0;
-      }
-    }
-    __syncthreads();
+  auto global_add = [&](uint32_t id, uint64_t pk, uint64_t by) {
+    atomicAdd((unsigned long long*)&c.cnt[2ull * id], (unsigned long long)pk);
+    atomicAdd((unsigned long long*)&c.cnt[2ull * id + 1], (unsigned long long)by);
   };
-  uint64_t running = 0;  // bytes added to the bins since the last flush (block-uniform)
-  constexpr int U = 4;    // records per thread per iteration (loads issued together)
+  uint64_t pk_run = 0, by_run = 0;  // this wave's adds since its last flush (wave-uniform)
   for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
     uint32_t s[U], len[U], id[U];
-    bool valid[U];
+    // streamed once: non-temporal, so the id map stays in L2
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
-      valid[k] = p < hi;
-      const uint64_t pc = valid[k] ? p : lo;  // unconditional loads
-      s[k] = c.acc_slot[pc];
-      len[k] = c.acc_len[pc];
-      if (!valid[k]) s[k] = 0xFFFFFFFFu, len[k] = 0;
+      const uint64_t pc = p < hi ? p : lo;  // unconditional loads
+      s[k] = __builtin_nontemporal_load(&c.acc_slot[pc]);
+      len[k] = __builtin_nontemporal_load(&c.acc_len[pc]);
+      if (p >= hi) s[k] = 0xFFFFFFFFu, len[k] = 0;
     }
+    if (c.sid) {
 #pragma unroll
-    for (int k = 0; k < U; ++k)
-      id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(c.meta[8ull * s[k] + 7] - 1);
+      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.sid[s[k]];
+    } else {
 #pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
-      if (c.out_id && valid[k] && p < c.out_cap) c.out_id[p] = id[k];
+      for (int k = 0; k < U; ++k)
+        id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(c.meta[8ull * s[k] + 7] - 1);
     }
-    uint64_t mysum = 0;
+    if (c.out_id) {
 #pragma unroll
-    for (int k = 0; k < U; ++k) mysum += id[k] != 0xFFFFFFFFu ? len[k] : 0u;
-    if (use_lds) {
-      const uint64_t ws = wave_sum64(mysum);
-      if (lane == 0) s_red[wave] = ws;
-      __syncthreads();
-      uint64_t chunk = 0;
-#pragma unroll
-      for (int w = 0; w < kCountBlock / 64; ++w) chunk += s_red[w];
-      if (running + chunk >= 0xFFFFFFFFull) {  // block-uniform decision
-        flush();
-        running = 0;
+      for (int k = 0; k < U; ++k) {
+        const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
+        if (p < hi && p < c.out_cap) __builtin_nontemporal_store(id[k], &c.out_id[p]);
       }
-      running += chunk;
+    }
+    if (use_lds) {
+      uint64_t mine_pk = 0, mine_by = 0;
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const bool ok = id[k] != 0xFFFFFFFFu && len[k] < kBigLen;
+        mine_pk += ok;
+        mine_by += ok ? len[k] : 0u;
+      }
+      const uint64_t it_pk = wave_sum64(mine_pk), it_by = wave_sum64(mine_by);
+      if (pk_run + it_pk >= c.wave_pk_budget || by_run + it_by >= kWaveByBudget) {
+        for (uint32_t b = lane; b < nflows; b += 64) {  // wave-local flush
+          const uint64_t v = __hip_atomic_exchange(&s_bin[b], 0ull, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (v) global_add(b, v >> kBinPkShift, v & kBinByMask);
+        }
+        pk_run = by_run = 0;
+      }
+      pk_run += it_pk;
+      by_run += it_by;
     }
 #pragma unroll
     for (int k = 0; k < U; ++k) {
@@ -990,31 +1044,71 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
       const uint64_t am = __ballot(mine);
       const uint32_t leader = am ? (uint32_t)__ffsll((unsigned long long)am) - 1 : 0u;
       const uint32_t id0 = __shfl(id[k], leader);
-      const bool uniform = __all(!mine || id[k] == id0);
-      const uint64_t bs = uniform ? wave_sum64(mine ? (uint64_t)len[k] : 0ull) : 0ull;
-      if (!use_lds) {
-        if (uniform) {
-          if (am && lane == leader) {
-            atomicAdd((unsigned long long*)&c.cnt[2ull * id0], (unsigned long long)__popcll(am));
-            atomicAdd((unsigned long long*)&c.cnt[2ull * id0 + 1], (unsigned long long)bs);
-          }
-        } else if (mine) {
-          atomicAdd((unsigned long long*)&c.cnt[2ull * id[k]], 1ull);
-          atomicAdd((unsigned long long*)&c.cnt[2ull * id[k] + 1], (unsigned long long)len[k]);
-        }
-      } else if (uniform) {
+      const bool big = mine && len[k] >= kBigLen;
+      const bool uniform = __all(!mine || id[k] == id0) && !__any(big);
+      if (uniform) {
+        const uint64_t bs = wave_sum64(mine ? (uint64_t)len[k] : 0ull);
         if (am && lane == leader) {
-          atomicAdd(&s_pk[id0], (uint32_t)__popcll(am));
-          atomicAdd(&s_by[id0], (uint32_t)bs);
+          if (use_lds)
+            atomicAdd((unsigned long long*)&s_bin[id0],
+                      ((unsigned long long)__popcll(am) << kBinPkShift) | bs);
+          else
+            global_add(id0, (uint64_t)__popcll(am), bs);
         }
       } else if (mine) {
-        atomicAdd(&s_pk[id[k]], 1u);
-        atomicAdd(&s_by[id[k]], len[k]);
+        if (use_lds && !big)
+          atomicAdd((unsigned long long*)&s_bin[id[k]], (1ull << kBinPkShift) | len[k]);
+        else
+          global_add(id[k], 1, len[k]);
       }
     }
-    if (use_lds) __syncthreads();  // s_red reuse
   }
-  if (use_lds) flush();
+  if (use_lds) {
+    // per-block partial histogram, dense and coalesced; k_count_reduce sums them
+    // (one writer per flow: no device-scope atomics, which cost ~40 ns each when
+    // every block flushes every flow)
+    __syncthreads();
+    if (c.part) {
+      uint64_t* part = c.part + (uint64_t)blockIdx.x * kCountBins;
+      for (uint32_t b = tid; b < nflows; b += kCountBlock) part[b] = s_bin[b];
+    } else {
+      for (uint32_t b = tid; b < nflows; b += kCountBlock) {
+        const uint64_t v = s_bin[b];
+        if (v) global_add(b, v >> kBinPkShift, v & kBinByMask);
+      }
+    }
+  }
+}
+
+// K3b: cnt[flow] += sum over K3 blocks of their packed partial bins.
+__global__ void k_count_reduce(CountArgs c, uint32_t nblocks) {
+  const uint64_t nflows = c.batch->flow_total;
+  if (nflows > (uint64_t)kCountBins) return;  // K3 used global atomics
+  for (uint64_t f = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; f < nflows;
+       f += (uint64_t)gridDim.x * blockDim.x) {
+    // 8 independent rows per step: the loads of a thread are in flight together
+    uint64_t pk = 0, by = 0;
+    uint32_t b = 0;
+    for (; b + 8 <= nblocks; b += 8) {
+      uint64_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = c.part[(uint64_t)(b + k) * kCountBins + f];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        pk += v[k] >> kBinPkShift;
+        by += v[k] & kBinByMask;
+      }
+    }
+    for (; b < nblocks; ++b) {
+      const uint64_t v = c.part[(uint64_t)b * kCountBins + f];
+      pk += v >> kBinPkShift;
+      by += v & kBinByMask;
+    }
+    if (pk) {
+      c.cnt[2 * f] += pk;
+      c.cnt[2 * f + 1] += by;
+    }
+  }
 }
 
 __global__ void k_finalize(BatchState* b, PersistState* p, uint64_t out_cap, uint64_t* out_n,
@@ -1231,6 +1325,7 @@ hipError_t launch_rank(const RankArgs& r, hipStream_t s) {
 
 hipError_t launch_count(const CountArgs& c, unsigned grid, hipStream_t s) {
   hipLaunchKernelGGL(k_count, dim3(grid), dim3(kCountBlock), 0, s, c);
+  if (c.part) hipLaunchKernelGGL(k_count_reduce, dim3(kCountBins / 256), dim3(256), 0, s, c, grid);
   return hipGetLastError();
 }
 

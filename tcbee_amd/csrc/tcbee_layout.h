@@ -28,6 +28,9 @@ constexpr uint8_t kTcpProtocol = 6;
 constexpr uint32_t kEthHdrLen = 14, kIpHdrLen = 20, kIp6HdrLen = 40, kTcpHdrLen = 20;
 constexpr uint32_t kV4MinLen = kEthHdrLen + kIpHdrLen + kTcpHdrLen;   // 54
 constexpr uint32_t kV6MinLen = kEthHdrLen + kIp6HdrLen + kTcpHdrLen;  // 74
+// Frame bytes the record and key are built from: ethertype (12) .. TCP checksum
+// (v4: 34+17 = 51, v6: 54+17 = 71). The MACs and the urgent pointer are never read.
+constexpr uint32_t kFirstUsedByte = 12, kV4LastUsedByte = 51, kV6LastUsedByte = 71;
 
 // record field offsets (bincode order of tcp_header.rs:554-572)
 constexpr int kRecTime = 0, kRecSaddr = 8, kRecDaddr = 12, kRecSaddrV6 = 16,

@@ -198,6 +198,19 @@ def test_lookback_recount_fallback(gpu, oracle, every, monkeypatch):
         assert p.status() == 0
 
 
+@pytest.mark.parametrize("budget,n,flows", [("64", 200_000, 300), ("1", 100_000, 3),
+                                            ("700", 400_000, 5000)])
+def test_k3_wave_flush_path(gpu, oracle, budget, n, flows, monkeypatch):
+    """K3's wave-local LDS-bin flush (atomic exchange under concurrent adds) forced
+    on every iteration: per-flow pkts/bytes stay exact."""
+    from tracegen import mixed_trace
+    monkeypatch.setenv("TCBEE_TEST_K3_BUDGET", budget)
+    tr = mixed_trace(n, seed=93, n_flows=flows)
+    with tcbee_amd.PacketParser(max_frames=1 << 19, max_arena=1 << 27, max_flows=1 << 14) as p:
+        assert_same(p.parse(tr), oracle.parse(tr), p.flows())
+        assert p.status() == 0
+
+
 @pytest.mark.parametrize("cuts", [[0, 30_000], [0, 9_000, 9_001, 21_000, 30_000],
                                   [0, 3_000, 6_000, 9_000, 12_000, 15_000, 18_000, 21_000, 30_000]])
 def test_device_merge_matches_unsharded(gpu, oracle, cuts):

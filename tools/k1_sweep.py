@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--fpl", default="1,2,4")
     ap.add_argument("--workloads", default="imix10k,imix1,64B1")
+    ap.add_argument("--var", default="", help="extra env A/B, e.g. TCBEE_K3_ATOMIC=0,1")
+    ap.add_argument("--flows-only", action="store_true", help="only the flows-on variants")
     args = ap.parse_args()
     import torch
     import tcbee_amd
@@ -46,11 +48,17 @@ def main():
         d_id = torch.empty(n, dtype=torch.int32, device="cuda")
         d_n = torch.zeros(1, dtype=torch.int64, device="cuda")
         d_ctr = torch.zeros(4, dtype=torch.int64, device="cuda")
-        variants = list(itertools.product(args.fpl.split(","), [True, False]))
+        var_name, _, var_vals = args.var.partition("=")
+        vvals = var_vals.split(",") if var_name else [""]
+        variants = list(itertools.product(args.fpl.split(","),
+                                          [True] if args.flows_only else [True, False], vvals))
         parsers = {}
-        for fpl, flows in variants:
+        for fpl, flows, vv in variants:
             os.environ["TCBEE_FPL"] = fpl
-            parsers[(fpl, flows)] = tcbee_amd.PacketParser(max_frames=n, max_flows=max(4 * nf, 4096))
+            if var_name:
+                os.environ[var_name] = vv
+            parsers[(fpl, flows, vv)] = tcbee_amd.PacketParser(max_frames=n,
+                                                               max_flows=max(4 * nf, 4096))
         times = {v: [] for v in variants}
         k1 = {v: [] for v in variants}
         for r in range(args.rounds):
@@ -74,7 +82,7 @@ def main():
                 times[v].append(el * 1e3)
                 k1[v].append(ms / max(k, 1))
         for v in variants:
-            key = f"{wl} fpl={v[0]} flows={int(v[1])}"
+            key = f"{wl} fpl={v[0]} flows={int(v[1])}" + (f" {var_name}={v[2]}" if var_name else "")
             step_ms = float(np.median(times[v]))
             k1_ms = float(np.median(k1[v]))
             results[key] = {"step_ms": round(step_ms, 4), "k1_ms": round(k1_ms, 4),
