@@ -21,9 +21,9 @@ struct tcbee_ctx {
   int fpl = 2;
   bool reset_pending = false;   // tcbee_flow_reset_device: applied by the next launch
   uint32_t withhold_every = 0;  // TCBEE_TEST_WITHHOLD (look-back recount test hook)
-  uint64_t k3_pk_budget = 0;    // TCBEE_TEST_K3_BUDGET (K3 wave-flush test hook)
-  int k3_atomic_flush = 0;      // TCBEE_K3_ATOMIC=1: K3 flushes bins with device atomics (A/B)
-  int k3_meta_gather = 0;       // TCBEE_K3_META=1: K3 gathers ids from the 64-B entries (A/B)
+  int k3_no_bucket = 0;         // TCBEE_TEST_K3_NOBUCKET=1: large tables use K3 mode 2 (test hook)
+  int k3_variant = 0;
+  uint32_t plain_walk = kPlainWalk;  // TCBEE_WALK: K1 plain probe walk length (A/B)           // TCBEE_K3ABL: timing-only K3 ablations / tilings (A/B)
 
   FlowTable tab{};
   uint64_t nslots = 0;
@@ -37,7 +37,12 @@ struct tcbee_ctx {
   uint32_t* d_bprefix = nullptr;
   uint32_t* d_slot_scratch = nullptr;
   uint32_t* d_len_scratch = nullptr;
-  uint64_t* d_count_part = nullptr;  // K3 per-block partial bins [n_cu][kCountBins]
+  uint64_t* d_count_part = nullptr;  // K3 mode 0 per-block partial bins [k3_g1max][kCountBins]
+  uint64_t* d_k3_region = nullptr;   // K3 mode 1 (tables with > kCountBins slots only)
+  uint32_t* d_k3_offs = nullptr;
+  uint64_t* d_k3_lpart = nullptr;
+  uint32_t k3_nb_max = 0, k3_g2 = 0;
+  uint64_t k3_g1max = 0;
   int n_cu = 256;
   uint64_t max_words = 0, max_sblocks = 0;
 
@@ -147,7 +152,7 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   dfree(c->tab.meta);
   dfree(c->tab.cnt);
-  dfree(c->tab.sid);
+  dfree(c->tab.cmap);
   dfree(c->d_persist);
   dfree(c->d_batch);
   dfree(c->d_tile_status);
@@ -158,6 +163,9 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
   dfree(c->d_slot_scratch);
   dfree(c->d_len_scratch);
   dfree(c->d_count_part);
+  dfree(c->d_k3_region);
+  dfree(c->d_k3_offs);
+  dfree(c->d_k3_lpart);
   dfree(c->d_arena);
   dfree(c->d_off);
   dfree(c->d_len);
@@ -191,9 +199,9 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   c->max_arena = max_arena;
   c->max_flows = max_flows < 16 ? 16 : max_flows;
   if (const char* e = std::getenv("TCBEE_TEST_WITHHOLD")) c->withhold_every = (uint32_t)std::atoi(e);
-  if (const char* e = std::getenv("TCBEE_TEST_K3_BUDGET")) c->k3_pk_budget = std::strtoull(e, nullptr, 10);
-  if (const char* e = std::getenv("TCBEE_K3_ATOMIC")) c->k3_atomic_flush = std::atoi(e);
-  if (const char* e = std::getenv("TCBEE_K3_META")) c->k3_meta_gather = std::atoi(e);
+  if (const char* e = std::getenv("TCBEE_TEST_K3_NOBUCKET")) c->k3_no_bucket = std::atoi(e);
+  if (const char* e = std::getenv("TCBEE_K3ABL")) c->k3_variant = std::atoi(e);
+  if (const char* e = std::getenv("TCBEE_WALK")) c->plain_walk = (uint32_t)std::atoi(e);
   if (const char* e = std::getenv("TCBEE_FPL")) {
     const int v = std::atoi(e);
     if (v == 1 || v == 2 || v == 4) c->fpl = v;
@@ -215,7 +223,7 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   hipError_t e = hipSuccess;
   if ((e = dalloc(&c->tab.meta, 8 * c->nslots)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.cnt, 2 * c->nslots)) != hipSuccess) return fail(map_err(e));
-  if ((e = dalloc(&c->tab.sid, c->nslots)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->tab.cmap, c->nslots)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_persist, 1)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_batch, 1)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_tile_status, c->max_tiles)) != hipSuccess) return fail(map_err(e));
@@ -228,9 +236,24 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->n_cu = prop.multiProcessorCount;
-  // K3's grid is at most n_cu blocks (launch site), one partial-bin row each
-  if ((e = dalloc(&c->d_count_part, (uint64_t)c->n_cu * kCountBins)) != hipSuccess)
+  // K3's grid (launch site): at most max(n_cu, blocks for < 2^24 records each),
+  // one partial-bin row each
+  c->k3_g1max = (max_frames + kK3MaxPer - 1) / kK3MaxPer;
+  if (c->k3_g1max < (uint64_t)c->n_cu) c->k3_g1max = c->n_cu;
+  if ((e = dalloc(&c->d_count_part, c->k3_g1max * kCountBins)) != hipSuccess)
     return fail(map_err(e));
+  if (c->nslots > (uint64_t)kCountBins && !c->k3_no_bucket) {
+    // K3 mode 1 scratch: (claim, caplen) per frame, bucket offsets per K3 block,
+    // partial rows of k_count_bucket (S x nb <= g2 rows of kBucket claims)
+    uint64_t nb = (c->nslots + kBucket - 1) / kBucket;
+    c->k3_nb_max = (uint32_t)(nb < kMaxBuckets ? nb : kMaxBuckets);
+    c->k3_g2 = c->k3_nb_max > 2u * c->n_cu ? c->k3_nb_max : 2u * c->n_cu;
+    if ((e = dalloc(&c->d_k3_region, max_frames)) != hipSuccess) return fail(map_err(e));
+    if ((e = dalloc(&c->d_k3_offs, c->k3_g1max * (c->k3_nb_max + 1))) != hipSuccess)
+      return fail(map_err(e));
+    if ((e = dalloc(&c->d_k3_lpart, 2ull * c->k3_g2 * kBucket)) != hipSuccess)
+      return fail(map_err(e));
+  }
   rc = tcbee_flow_reset(c);
   if (rc != TCBEE_OK) return fail(rc);
   *out = c;
@@ -318,7 +341,7 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     a.out_rec = out_rec74;
     a.out_cap = out_cap;
     a.out_hash = flows ? out_flow_hash : nullptr;
-    a.acc_slot = c->d_slot_scratch;
+    a.acc_flow = c->d_slot_scratch;
     a.acc_len = c->d_len_scratch;
     a.tile_status = c->d_tile_status;
     a.ntiles = ntiles;
@@ -328,6 +351,7 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     a.tab = c->tab;
     a.filter_port = cfg->filter_port;
     a.withhold_every = c->withhold_every;
+    a.plain_walk = c->plain_walk;
     const bool timed = c->profiling && c->ev_used < kMaxProfiled;
     if (timed) TRY_HIP(hipEventRecord(c->ev[2 * c->ev_used], s));
     TRY_HIP(launch_parse(a, fpl, flows, s));
@@ -353,23 +377,29 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     k.ctr = ctr_dev;
     k.direction = cfg->direction;
     k.persist_rw = c->d_persist;
-    k.acc_slot = c->d_slot_scratch;
+    k.acc_flow = c->d_slot_scratch;
     k.acc_len = c->d_len_scratch;
     k.out_id = out_flow_id;
     k.out_cap = out_cap;
     k.batch = c->d_batch;
     k.persist = c->d_persist;
-    k.meta = c->tab.meta;
-    k.sid = c->k3_meta_gather ? nullptr : c->tab.sid;
+    k.cmap = c->tab.cmap;
     k.cnt = c->tab.cnt;
-    k.part = c->k3_atomic_flush ? nullptr : c->d_count_part;
-    k.wave_pk_budget = c->k3_pk_budget && c->k3_pk_budget < kWavePkBudget ? c->k3_pk_budget
-                                                                           : kWavePkBudget;
-    // trade-off: more blocks = more latency hidden; each block flushes every bin it
-    // touched, so a block should see a few thousand records
-    const uint64_t want = (in->n + 8191) / 8192;
-    const unsigned grid = (unsigned)(want < (uint64_t)c->n_cu ? (want ? want : 1) : c->n_cu);
-    TRY_HIP(launch_count(k, grid, s));  // finalize is folded into its block 0
+    k.part = c->d_count_part;
+    k.region = c->d_k3_region;
+    k.offs = c->d_k3_offs;
+    k.nb_max = c->k3_nb_max;
+    k.lpart = c->d_k3_lpart;
+    // trade-off: more blocks = more latency hidden; each block writes a partial row
+    // of every flow, so a block should see a few thousand records; and a block
+    // never covers more than kK3MaxPer records (bin fields cannot overflow)
+    uint64_t g1 = (in->n + 8191) / 8192;
+    if (g1 > (uint64_t)c->n_cu) g1 = c->n_cu;
+    const uint64_t gmin = (in->n + kK3MaxPer - 1) / kK3MaxPer;
+    if (g1 < gmin) g1 = gmin;
+    if (g1 == 0) g1 = 1;
+    // finalize is folded into k_count's block 0
+    TRY_HIP(launch_count(k, (unsigned)g1, c->d_k3_region ? c->k3_g2 : 0u, s, c->k3_variant));
   } else {
     TRY_HIP(launch_finalize(c->d_batch, c->d_persist, out_cap, out_n_dev, ctr_dev, cfg->direction, s));
   }

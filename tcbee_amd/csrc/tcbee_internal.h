@@ -11,7 +11,9 @@ namespace tcbee {
 constexpr uint32_t kStFlowFull = 1u, kStSpin = 2u;
 
 // Flow table in HBM, open addressing, linear probing, power-of-two slots.
-//  meta[s*8 + 0] tag   (0 empty, 1 busy, else hash_tag(h))
+//  meta[s*8 + 0] tag word: 0 empty, 1 busy, else hash_tag32(h) | claim << 32,
+//                      claim = the flow's dense claim index (insertion order over
+//                      the context's life, fixed at insert; cmap[claim] = dense id)
 //  meta[s*8 + 1..5]    the 40-B key as 5 LE u64 words
 //  meta[s*8 + 6]       first_seen (global accepted-frame index, ~0 = none)
 //  meta[s*8 + 7]       dense flow id + 1 (0 = not yet assigned)
@@ -21,8 +23,8 @@ struct FlowTable {
   uint64_t* meta;
   uint64_t* cnt;
   uint64_t mask;  // slots - 1
-  uint32_t* sid;  // slot -> dense id (0-based), valid once meta[7] != 0; K3's compact
-                  // gather source (4 B per slot instead of a 64-B entry)
+  uint32_t* cmap;  // claim index -> dense id (0-based), written by K2; dense in
+                   // [0, flows), so K3 stages it in LDS
 };
 
 // Lives across batches of one context.
@@ -65,7 +67,7 @@ struct ParseArgs {
   uint8_t* out_rec;
   uint64_t out_cap;
   uint32_t* out_hash;
-  uint32_t* acc_slot;     // per accepted frame: flow-table slot (ctx scratch)
+  uint32_t* acc_flow;     // per accepted frame: the flow's claim index (ctx scratch)
   uint32_t* acc_len;      // per accepted frame: caplen (ctx scratch)
   uint64_t* tile_status;  // decoupled look-back words, one per tile
   uint64_t ntiles;
@@ -75,7 +77,9 @@ struct ParseArgs {
   FlowTable tab;
   uint16_t filter_port;
   uint32_t withhold_every;  // test hook (TCBEE_TEST_WITHHOLD): 0 in production
+  uint32_t plain_walk;      // probe steps past foreign slots with plain loads (kPlainWalk)
 };
+constexpr uint32_t kPlainWalk = 8;
 
 struct RankArgs {
   const uint64_t* new_list;
@@ -98,20 +102,23 @@ struct CountArgs {
   tcbee_counters* ctr;
   int direction;
   PersistState* persist_rw;
-  const uint32_t* acc_slot;
+  const uint32_t* acc_flow;
   const uint32_t* acc_len;
   uint32_t* out_id;
   uint64_t out_cap;
   const BatchState* batch;
   const PersistState* persist;
-  const uint64_t* meta;
-  const uint32_t* sid;       // nullptr: gather ids from meta (A/B, TCBEE_K3_META=1)
+  const uint32_t* cmap;      // claim index -> dense id
   uint64_t* cnt;
-  uint64_t wave_pk_budget;   // records a wave adds to the LDS bins between its flushes
-  uint64_t* part;            // [gridDim.x][kCountBins] per-block packed bins (LDS path);
-                             // nullptr: flush the bins with device atomics instead
+  uint64_t* part;            // mode 0: [g1][kCountBins] per-block packed bins
+  // mode 1 (large tables; region == nullptr disables it)
+  uint64_t* region;          // per accepted frame: (claim, caplen), bucket-sorted per block
+  uint32_t* offs;            // [g1][nb_max + 1] bucket offsets inside each block's region
+  uint32_t nb_max;           // buckets the context's table can need
+  uint64_t* lpart;           // [S][nb * kBucket][2] partial pkts/bytes per claim
 };
-hipError_t launch_count(const CountArgs& c, unsigned grid, hipStream_t s);
+// g1 = k_count blocks; g2 = k_count_bucket blocks (0: mode 1 impossible, not launched)
+hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g2, hipStream_t s, int k3v = 0);
 
 struct MergeArgs {
   const uint64_t* ent;        // nseg * stride entries, tcbee_flow_entry as u64[8]
@@ -140,9 +147,14 @@ constexpr int kBlock = 256;
 constexpr int kScanWordsPerBlock = 2048;  // 256 threads x 8 words
 constexpr uint64_t kRankSmallWords = 1024 * 32;  // single-block rank up to 1M frames
 constexpr int kCountBlock = 1024;
-constexpr int kCountBins = 16384;         // 128 KiB of LDS (u64 bins)
+constexpr int kCountBins = 12288;         // 96 KiB of u64 bins + 48 KiB claim->id map in LDS
 constexpr int kBinPkShift = 40;           // K3 bin: pkts in bits 63:40, bytes in 39:0
-constexpr uint64_t kWavePkBudget = (1ull << (64 - kBinPkShift)) / (kCountBlock / 64);  // 2^20
-constexpr uint64_t kWaveByBudget = (1ull << kBinPkShift) / (kCountBlock / 64);         // 2^36
+constexpr uint32_t kBigLen = 1u << 16;    // caplen >= 64 KiB: counted by device atomics
+// a K3 block covers at most kK3MaxPer records (a multiple of the range granule),
+// so a bin's pkts (< 2^24) and bytes (< 2^24 * kBigLen = 2^40) never overflow
+constexpr uint64_t kK3Gran = 16384;
+constexpr uint64_t kK3MaxPer = (1ull << 24) - kK3Gran;
+constexpr int kBucketBits = 12, kBucket = 1 << kBucketBits;  // claims per mode-1 bucket
+constexpr uint32_t kMaxBuckets = 4096;    // mode 1 up to 16M flows (hist + cursors: 32 KiB)
 
 }  // namespace tcbee

@@ -294,10 +294,13 @@ __device__ __forceinline__ bool fs_needs_min(uint64_t fs_seen, uint64_t frame_i,
   return gidx < fs_seen;
 }
 
+// Returns the slot (~0 on failure); `claim` = the flow's claim index (tag word
+// bits 63:32): flow_count before this batch + its position in this batch's
+// new-flow list, fixed before the tag is published.
 __device__ uint32_t flow_upsert(const FlowTable& T, const uint64_t (&K)[5], uint64_t h,
                                 BatchState* batch, uint64_t* new_list, PersistState* persist,
-                                uint64_t& fs_seen, uint64_t claim_mark = ~0ull) {
-  const uint64_t tag = hash_tag(h);
+                                uint64_t& fs_seen, uint32_t& claim, uint64_t claim_mark = ~0ull) {
+  const uint32_t tag = hash_tag32(h);
   uint64_t s = h & T.mask;
   for (uint64_t probe = 0; probe <= T.mask; ++probe) {
     uint64_t* m = T.meta + s * 8;
@@ -306,13 +309,14 @@ __device__ uint32_t flow_upsert(const FlowTable& T, const uint64_t (&K)[5], uint
       uint64_t expected = kTagEmpty;
       if (__hip_atomic_compare_exchange_strong(m, &expected, kTagBusy, __ATOMIC_RELAXED,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        const uint64_t slot_no = atomicAdd((unsigned long long*)&batch->n_new, 1ull);
+        new_list[slot_no] = s;
+        claim = (uint32_t)(persist->flow_count + slot_no);
 #pragma unroll
         for (int j = 0; j < 5; ++j) st_agent(m + 1 + j, K[j]);
         st_agent(m + 6, claim_mark);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        st_agent(m, tag);
-        const uint64_t slot_no = atomicAdd((unsigned long long*)&batch->n_new, 1ull);
-        new_list[slot_no] = s;
+        st_agent(m, (uint64_t)tag | ((uint64_t)claim << 32));
         fs_seen = claim_mark;
         return (uint32_t)s;
       }
@@ -326,7 +330,7 @@ __device__ uint32_t flow_upsert(const FlowTable& T, const uint64_t (&K)[5], uint
       __builtin_amdgcn_s_sleep(1);
       cur = ld_agent(m);
     }
-    if (cur == tag) {
+    if ((uint32_t)cur == tag) {
       bool eq = true;
 #pragma unroll
       for (int j = 0; j < 5; ++j) eq = eq && (ld_agent(m + 1 + j) == K[j]);
@@ -337,6 +341,7 @@ __device__ uint32_t flow_upsert(const FlowTable& T, const uint64_t (&K)[5], uint
       }
       if (eq) {
         fs_seen = ld_agent(m + 6);
+        claim = (uint32_t)(cur >> 32);
         return (uint32_t)s;
       }
     }
@@ -526,7 +531,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
 
   uint32_t R[FPL][19];
   bool acc[FPL];
-  uint32_t rank[FPL], slot[FPL], hsh[FPL], clen[FPL];
+  uint32_t rank[FPL], slot[FPL], hsh[FPL], clen[FPL], claim[FPL];
   uint64_t fs_seen[FPL];
   uint64_t K[FPL][5];
 
@@ -538,6 +543,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
     const uint64_t i = i0 + (uint64_t)f * kBlock + tid;
     acc[f] = false;
     slot[f] = 0xFFFFFFFFu;
+    claim[f] = 0xFFFFFFFFu;
     hsh[f] = 0;
     fs_seen[f] = ~0ull;
 #pragma unroll
@@ -626,24 +632,62 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
     // phase C: resolve; a miss (new flow, collision, busy slot) takes the full upsert
 #pragma unroll
     for (int f = 0; f < FPL; ++f) {
-      uint32_t sl = 0xFFFFFFFFu;
+      uint32_t sl = 0xFFFFFFFFu, cl = 0xFFFFFFFFu;
       uint64_t fs = ~0ull;
       if (want[f]) {
-        const bool hit = W[f][0] == hash_tag(h[f]) && W[f][1] == K[f][0] && W[f][2] == K[f][1] &&
-                         W[f][3] == K[f][2] && W[f][4] == K[f][3] && W[f][5] == K[f][4];
+        const bool hit = (uint32_t)W[f][0] == hash_tag32(h[f]) && W[f][1] == K[f][0] &&
+                         W[f][2] == K[f][1] && W[f][3] == K[f][2] && W[f][4] == K[f][3] &&
+                         W[f][5] == K[f][4];
         if (hit) {
           sl = (uint32_t)(h[f] & a.tab.mask);
           fs = W[f][6];
+          cl = (uint32_t)(W[f][0] >> 32);
         } else {
-          sl = flow_upsert(a.tab, K[f], h[f], a.batch, a.new_list, a.persist, fs,
-                           kFsFlag | (i0 + (uint64_t)f * kBlock + tid));
+          // Walk on with plain loads while the slots hold OTHER flows (a published
+          // tag word of another hash; a tag equal to ours with another key goes to
+          // the coherent path). Within a batch a slot only
+          // goes EMPTY -> BUSY -> published, so a published foreign slot seen in
+          // any snapshot is foreign for good; EMPTY/BUSY may be stale and end the
+          // walk. Collisions of existing flows thus stay off the atomic path.
+          const uint32_t mytag = hash_tag32(h[f]);
+          uint64_t s = h[f] & a.tab.mask;
+          uint64_t cur0 = W[f][0];
+          bool slow = true;
+          for (uint32_t step = 0; step < a.plain_walk; ++step) {
+            if (cur0 < 2 || (uint32_t)cur0 == mytag) break;
+            s = (s + 1) & a.tab.mask;
+            u32x4 q[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              q[j] = __builtin_amdgcn_raw_buffer_load_b128(meta_rs, (uint32_t)(s * 64u) + 16u * j, 0, PROBE_AUX);
+            uint64_t V[7];
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+              const u32x4 v = q[j >> 1];
+              V[j] = (j & 1) ? ((uint64_t)v[2] | ((uint64_t)v[3] << 32)) : ((uint64_t)v[0] | ((uint64_t)v[1] << 32));
+            }
+            cur0 = V[0];
+            if ((uint32_t)V[0] == mytag && V[1] == K[f][0] && V[2] == K[f][1] && V[3] == K[f][2] &&
+                V[4] == K[f][3] && V[5] == K[f][4]) {
+              sl = (uint32_t)s;
+              fs = V[6];
+              cl = (uint32_t)(V[0] >> 32);
+              slow = false;
+              break;
+            }
+          }
+          if (slow)
+            sl = flow_upsert(a.tab, K[f], h[f], a.batch, a.new_list, a.persist, fs, cl,
+                             kFsFlag | (i0 + (uint64_t)f * kBlock + tid));
         }
       }
       if (uni[f]) {
         slot[f] = __shfl(sl, leader[f]);
+        claim[f] = __shfl(cl, leader[f]);
         fs_seen[f] = __shfl(fs, leader[f]);
       } else if (acc[f]) {
         slot[f] = sl;
+        claim[f] = sl == 0xFFFFFFFFu ? 0xFFFFFFFFu : cl;
         fs_seen[f] = fs;
       }
     }
@@ -705,7 +749,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
     if (acc[f] && !(ABL & 16)) {
       if (a.out_hash && p < a.out_cap) st_stream<NT>(a.out_hash + p, hsh[f]);
       if (FLOWS) {
-        st_stream<NT>(a.acc_slot + p, slot[f]);
+        st_stream<NT>(a.acc_flow + p, claim[f]);
         st_stream<NT>(a.acc_len + p, clen[f]);
       }
     }
@@ -803,7 +847,7 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
       }
       const uint64_t sl = r.new_list[j];
       r.tab.meta[8 * sl + 7] = fbase + rank + 1;
-      r.tab.sid[sl] = (uint32_t)(fbase + rank);
+      r.tab.cmap[fbase + j] = (uint32_t)(fbase + rank);
     }
     return;
   }
@@ -858,7 +902,7 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
     const uint32_t below = __hip_atomic_load(&r.bitmap[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
                            ((1u << (local & 31)) - 1u);
     r.tab.meta[8 * s + 7] = fbase + r.wprefix[w] + __popc(below) + 1;
-    r.tab.sid[s] = (uint32_t)(fbase + r.wprefix[w] + __popc(below));
+    r.tab.cmap[fbase + j] = (uint32_t)(fbase + r.wprefix[w] + __popc(below));
   }
 }
 
@@ -939,28 +983,140 @@ __global__ void k_assign(RankArgs r) {
     const uint32_t below = r.bitmap[w] & ((1u << (local & 31)) - 1u);
     const uint64_t id = fbase + r.bprefix[w / kScanWordsPerBlock] + r.wprefix[w] + __popc(below);
     r.tab.meta[8 * s + 7] = id + 1;
-    r.tab.sid[s] = (uint32_t)id;
+    r.tab.cmap[fbase + j] = (uint32_t)id;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) r.batch->flow_total = fbase + n_new;
 }
 
-// K3: per accepted frame, slot -> dense id (written for records p < out_cap) and
-// pkts/bytes per flow. While every flow fits the LDS bins (<= kCountBins), each
-// block histograms a contiguous range of accepted frames in LDS — one 64-bit
-// bin per flow, pkts in bits 63:40 and bytes in bits 39:0, one LDS atomic per
-// record (one per wave when the wave's records share a flow) — and flushes the
-// non-zero bins with one global atomic pair each at the end. No block barrier
-// inside the loop: each wave tracks what it added since its last flush and,
-// before its share could overflow a bin field, flushes every bin itself with
-// atomic exchanges (exact under concurrent adds; never taken at realistic
-// sizes). Frames longer than 2^24 bytes go straight to global atomics.
-// With more flows than bins: per-frame global atomics (wave-uniform flows
-// aggregated first).
+// K3: per accepted frame, claim index -> dense id (written for records p <
+// out_cap) and pkts/bytes per flow. Three modes, chosen on the device from the
+// batch's flow count F (the host cannot know it without a sync):
+//  0  F <= kCountBins: each block histograms a contiguous range of accepted
+//     frames in LDS with the claim->id map staged beside the bins — one 64-bit
+//     bin per flow (pkts in bits 63:40, bytes in 39:0), one LDS atomic per record,
+//     one per wave-iteration when all of a wave's records share a flow — then
+//     writes its bins as a dense partial row that k_count_reduce sums. A block
+//     covers < 2^24 records and frames of >= kBigLen bytes go to global atomics,
+//     so no bin field can overflow (no flushes inside the loop).
+//  1  F <= nb_max * kBucket (the large-table path): claims are bucketed by
+//     claim >> kBucketBits. Each block counts its range's records per bucket,
+//     scans the counts, then scatters (claim, caplen) into its own region of a
+//     scratch buffer, bucket by bucket; k_count_bucket then histograms one bucket
+//     (from every block's segment of it) in LDS per workgroup; the reduce maps
+//     claims to ids. Replaces per-record device atomics (~86 ps per record at
+//     1M flows) with ~36 B of streaming traffic per record.
+//  2  otherwise (or no scratch): per-record global atomics, wave-uniform flows
+//     aggregated first.
 constexpr uint64_t kBinByMask = (1ull << kBinPkShift) - 1;
-constexpr uint32_t kBigLen = 1u << 24;
 
+__device__ __forceinline__ int count_mode(const CountArgs& c, uint64_t nflows) {
+  if (nflows <= (uint64_t)kCountBins) return 0;
+  if (c.region && nflows <= (uint64_t)c.nb_max * kBucket) return 1;
+  return 2;
+}
+
+// records [lo, hi) of K3 block `b` (identical in k_count and k_count_bucket)
+__device__ __forceinline__ uint64_t count_per(uint64_t n_acc, uint32_t grid) {
+  return ((n_acc + grid - 1) / grid + kK3Gran - 1) / kK3Gran * kK3Gran;
+}
+
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// exclusive scan over the 1024 threads of a block; s_w: 16 words of LDS
+__device__ __forceinline__ uint32_t block1024_excl_scan(uint32_t v, uint32_t* s_w, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) s_w[wave] = x;
+  __syncthreads();
+  uint32_t base = 0;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < kCountBlock / 64; ++w) {
+    const uint32_t t = s_w[w];
+    if ((uint32_t)w < wave) base += t;
+    total += t;
+  }
+  __syncthreads();
+  return base + x - v;
+}
+
+// Mode 1, phase 1 (inside k_count): ids out, bucket counts, scan, scatter.
+template <int U>
+__device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint64_t nflows,
+                              uint32_t* hist, uint32_t* cur, uint32_t* s_w) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);
+  for (uint32_t b = tid; b < nb; b += kCountBlock) hist[b] = 0;
+  __syncthreads();
+  for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
+    uint32_t s[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
+      s[k] = __builtin_nontemporal_load(&c.acc_flow[p < hi ? p : lo]);
+      if (p >= hi) s[k] = 0xFFFFFFFFu;
+    }
+    uint32_t id[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.cmap[s[k]];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
+      if (c.out_id && p < hi && p < c.out_cap) __builtin_nontemporal_store(id[k], &c.out_id[p]);
+      if (s[k] != 0xFFFFFFFFu) atomicAdd(&hist[s[k] >> kBucketBits], 1u);
+    }
+  }
+  __syncthreads();
+  // exclusive scan of hist[0, nb): thread t owns buckets [t*q, t*q + q)
+  const uint32_t q = (nb + kCountBlock - 1) / kCountBlock;
+  uint32_t mine = 0;
+  for (uint32_t b = tid * q; b < nb && b < (tid + 1) * q; ++b) mine += hist[b];
+  uint32_t total;
+  uint32_t run = block1024_excl_scan(mine, s_w, total);
+  uint32_t* offs = c.offs + (uint64_t)blockIdx.x * (c.nb_max + 1);
+  for (uint32_t b = tid * q; b < nb && b < (tid + 1) * q; ++b) {
+    cur[b] = run;
+    offs[b] = run;
+    run += hist[b];
+  }
+  if (tid == 0) offs[nb] = total;
+  __syncthreads();
+  for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
+    uint32_t s[U], len[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
+      const uint64_t pc = p < hi ? p : lo;
+      s[k] = __builtin_nontemporal_load(&c.acc_flow[pc]);
+      len[k] = __builtin_nontemporal_load(&c.acc_len[pc]);
+      if (p >= hi) s[k] = 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      if (s[k] != 0xFFFFFFFFu) {
+        const uint32_t pos = atomicAdd(&cur[s[k] >> kBucketBits], 1u);
+        c.region[lo + pos] = (uint64_t)s[k] | ((uint64_t)len[k] << 32);
+      }
+    }
+  }
+}
+
+// ABL3 (timing-only ablations, 0 in every product launch): 1 no bin updates,
+// 2 no id gather, 4 no id stores
+template <int U, int ABL3>
 __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   __shared__ uint64_t s_bin[kCountBins];
+  __shared__ uint32_t s_map[kCountBins];  // claim index -> dense id
+  __shared__ uint32_t s_w[kCountBlock / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint64_t n_acc = c.batch->n_acc;
   const uint64_t nflows = c.batch->flow_total;
@@ -977,139 +1133,208 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
     c.persist_rw->rec_base += n_acc;
     c.persist_rw->flow_count = nflows;
   }
-  constexpr int U = 8;  // records per thread per iteration (loads issued together)
-  const bool use_lds = nflows <= (uint64_t)kCountBins;
-  const uint64_t per = ((n_acc + gridDim.x - 1) / gridDim.x + U * kCountBlock - 1) /
-                       (U * kCountBlock) * (U * kCountBlock);
-  const uint64_t lo = (uint64_t)blockIdx.x * per;
+  const int mode = count_mode(c, nflows);
+  const uint64_t per = count_per(n_acc, gridDim.x);
+  const uint64_t lo = (uint64_t)blockIdx.x * per < n_acc ? (uint64_t)blockIdx.x * per : n_acc;
   const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
-  if (use_lds) {
-    for (uint32_t b = tid; b < nflows; b += kCountBlock) s_bin[b] = 0;
+  if (mode == 1) {
+    uint32_t* h = reinterpret_cast<uint32_t*>(s_bin);
+    count_scatter<U>(c, lo, hi, nflows, h, h + kMaxBuckets, s_w);
+    return;
+  }
+  if (mode == 0) {
+    for (uint32_t b = tid; b < nflows; b += kCountBlock) {
+      s_bin[b] = 0;
+      s_map[b] = c.cmap[b];
+    }
     __syncthreads();
   }
   auto global_add = [&](uint32_t id, uint64_t pk, uint64_t by) {
     atomicAdd((unsigned long long*)&c.cnt[2ull * id], (unsigned long long)pk);
     atomicAdd((unsigned long long*)&c.cnt[2ull * id + 1], (unsigned long long)by);
   };
-  uint64_t pk_run = 0, by_run = 0;  // this wave's adds since its last flush (wave-uniform)
   for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
     uint32_t s[U], len[U], id[U];
-    // streamed once: non-temporal, so the id map stays in L2
+    // streamed once: non-temporal
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
       const uint64_t pc = p < hi ? p : lo;  // unconditional loads
-      s[k] = __builtin_nontemporal_load(&c.acc_slot[pc]);
+      s[k] = __builtin_nontemporal_load(&c.acc_flow[pc]);
       len[k] = __builtin_nontemporal_load(&c.acc_len[pc]);
       if (p >= hi) s[k] = 0xFFFFFFFFu, len[k] = 0;
     }
-    if (c.sid) {
+    if (ABL3 & 2) {
 #pragma unroll
-      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.sid[s[k]];
+      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : (s[k] & 8191u);
+    } else if (mode == 0) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : s_map[s[k]];
     } else {
 #pragma unroll
-      for (int k = 0; k < U; ++k)
-        id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(c.meta[8ull * s[k] + 7] - 1);
+      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.cmap[s[k]];
     }
-    if (c.out_id) {
+    if (c.out_id && !(ABL3 & 4)) {
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
         if (p < hi && p < c.out_cap) __builtin_nontemporal_store(id[k], &c.out_id[p]);
       }
     }
-    if (use_lds) {
-      uint64_t mine_pk = 0, mine_by = 0;
+    if (ABL3 & 1) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int k = 0; k < U; ++k) x ^= id[k] ^ len[k];
+      asm volatile("" ::"v"(x));
+      continue;
+    }
+    if (mode == 0) {
+      // one flow in all of the wave's records this iteration (a hot flow): one add
+      const uint32_t id0 = __builtin_amdgcn_readfirstlane(id[0]);
+      bool same = id0 != 0xFFFFFFFFu;
+      uint32_t nk = 0, sl = 0;
 #pragma unroll
       for (int k = 0; k < U; ++k) {
-        const bool ok = id[k] != 0xFFFFFFFFu && len[k] < kBigLen;
-        mine_pk += ok;
-        mine_by += ok ? len[k] : 0u;
+        const bool v = id[k] != 0xFFFFFFFFu;
+        same = same && (!v || (id[k] == id0 && len[k] < kBigLen));
+        nk += v ? 1u : 0u;
+        sl += v ? len[k] : 0u;
       }
-      const uint64_t it_pk = wave_sum64(mine_pk), it_by = wave_sum64(mine_by);
-      if (pk_run + it_pk >= c.wave_pk_budget || by_run + it_by >= kWaveByBudget) {
-        for (uint32_t b = lane; b < nflows; b += 64) {  // wave-local flush
-          const uint64_t v = __hip_atomic_exchange(&s_bin[b], 0ull, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (v) global_add(b, v >> kBinPkShift, v & kBinByMask);
-        }
-        pk_run = by_run = 0;
-      }
-      pk_run += it_pk;
-      by_run += it_by;
-    }
+      if (__all(same)) {
+        // pk <= 64*U, by <= 64*U*(kBigLen-1) < 2^32
+        const uint32_t pk = wave_sum32(nk), by = wave_sum32(sl);
+        if (lane == 0)
+          atomicAdd((unsigned long long*)&s_bin[id0], ((unsigned long long)pk << kBinPkShift) | by);
+      } else {
 #pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const bool mine = id[k] != 0xFFFFFFFFu;
-      const uint64_t am = __ballot(mine);
-      const uint32_t leader = am ? (uint32_t)__ffsll((unsigned long long)am) - 1 : 0u;
-      const uint32_t id0 = __shfl(id[k], leader);
-      const bool big = mine && len[k] >= kBigLen;
-      const bool uniform = __all(!mine || id[k] == id0) && !__any(big);
-      if (uniform) {
-        const uint64_t bs = wave_sum64(mine ? (uint64_t)len[k] : 0ull);
-        if (am && lane == leader) {
-          if (use_lds)
-            atomicAdd((unsigned long long*)&s_bin[id0],
-                      ((unsigned long long)__popcll(am) << kBinPkShift) | bs);
+        for (int k = 0; k < U; ++k) {
+          if (id[k] == 0xFFFFFFFFu) continue;
+          if (len[k] < kBigLen)
+            atomicAdd((unsigned long long*)&s_bin[id[k]], (1ull << kBinPkShift) | len[k]);
           else
-            global_add(id0, (uint64_t)__popcll(am), bs);
+            global_add(id[k], 1, len[k]);
         }
-      } else if (mine) {
-        if (use_lds && !big)
-          atomicAdd((unsigned long long*)&s_bin[id[k]], (1ull << kBinPkShift) | len[k]);
-        else
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const bool mine = id[k] != 0xFFFFFFFFu;
+        const uint64_t am = __ballot(mine);
+        const uint32_t leader = am ? (uint32_t)__ffsll((unsigned long long)am) - 1 : 0u;
+        const uint32_t id0 = __shfl(id[k], leader);
+        if (__all(!mine || id[k] == id0)) {
+          const uint64_t bs = wave_sum64(mine ? (uint64_t)len[k] : 0ull);
+          if (am && lane == leader) global_add(id0, (uint64_t)__popcll(am), bs);
+        } else if (mine) {
           global_add(id[k], 1, len[k]);
+        }
       }
     }
   }
-  if (use_lds) {
+  if (mode == 0) {
     // per-block partial histogram, dense and coalesced; k_count_reduce sums them
-    // (one writer per flow: no device-scope atomics, which cost ~40 ns each when
-    // every block flushes every flow)
+    // (one writer per flow: no device-scope atomics)
     __syncthreads();
-    if (c.part) {
-      uint64_t* part = c.part + (uint64_t)blockIdx.x * kCountBins;
-      for (uint32_t b = tid; b < nflows; b += kCountBlock) part[b] = s_bin[b];
-    } else {
-      for (uint32_t b = tid; b < nflows; b += kCountBlock) {
-        const uint64_t v = s_bin[b];
-        if (v) global_add(b, v >> kBinPkShift, v & kBinByMask);
+    uint64_t* part = c.part + (uint64_t)blockIdx.x * kCountBins;
+    for (uint32_t b = tid; b < nflows; b += kCountBlock) part[b] = s_bin[b];
+  }
+}
+
+// Mode 1, phase 2: workgroup (j, s) histograms bucket j over the segments of K3
+// blocks s, s+S, ... (S = gridDim / nb) in LDS; each wave walks one block's
+// segment at a time, 4 records per lane in flight. Writes a dense partial row.
+__global__ __launch_bounds__(kCountBlock) void k_count_bucket(CountArgs c, uint32_t g1) {
+  __shared__ uint64_t s_pk[kBucket], s_by[kBucket];
+  const uint64_t nflows = c.batch->flow_total;
+  if (count_mode(c, nflows) != 1) return;
+  const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);
+  const uint32_t S = gridDim.x / nb;
+  const uint32_t j = blockIdx.x % nb, s = blockIdx.x / nb;
+  if (s >= S) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  for (uint32_t t = tid; t < kBucket; t += kCountBlock) s_pk[t] = s_by[t] = 0;
+  __syncthreads();
+  const uint64_t n_acc = c.batch->n_acc;
+  const uint64_t per = count_per(n_acc, g1);
+  constexpr uint32_t kWaves = kCountBlock / 64;
+  for (uint32_t q = s + S * wave; q < g1; q += S * kWaves) {
+    const uint64_t lo_q = (uint64_t)q * per;
+    if (lo_q >= n_acc) break;
+    const uint32_t* o = c.offs + (uint64_t)q * (c.nb_max + 1);
+    const uint64_t a0 = lo_q + o[j], a1 = lo_q + o[j + 1];
+    for (uint64_t x = a0 + lane; x < a1; x += 256) {
+      uint64_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        v[u] = x + 64u * u < a1 ? __builtin_nontemporal_load(&c.region[x + 64u * u]) : ~0ull;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (v[u] == ~0ull) continue;
+        const uint32_t t = (uint32_t)v[u] & (kBucket - 1);
+        atomicAdd((unsigned long long*)&s_pk[t], 1ull);
+        atomicAdd((unsigned long long*)&s_by[t], (unsigned long long)(v[u] >> 32));
+      }
+    }
+  }
+  __syncthreads();
+  uint64_t* lp = c.lpart + 2ull * ((uint64_t)s * nb * kBucket + (uint64_t)j * kBucket);
+  for (uint32_t t = tid; t < kBucket; t += kCountBlock) {
+    lp[2 * t] = s_pk[t];
+    lp[2 * t + 1] = s_by[t];
+  }
+}
+
+// K3 reduce: mode 0 sums the g1 packed partial rows per dense id; mode 1 sums
+// the S partial rows per claim and maps claims to ids. cnt is by dense id.
+__global__ void k_count_reduce(CountArgs c, uint32_t g1, uint32_t g2) {
+  const uint64_t nflows = c.batch->flow_total;
+  const int mode = count_mode(c, nflows);
+  const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  if (mode == 0) {
+    for (uint64_t f = t0; f < nflows; f += stride) {
+      // 8 independent rows per step: the loads of a thread are in flight together
+      uint64_t pk = 0, by = 0;
+      uint32_t b = 0;
+      for (; b + 8 <= g1; b += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = c.part[(uint64_t)(b + k) * kCountBins + f];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          pk += v[k] >> kBinPkShift;
+          by += v[k] & kBinByMask;
+        }
+      }
+      for (; b < g1; ++b) {
+        const uint64_t v = c.part[(uint64_t)b * kCountBins + f];
+        pk += v >> kBinPkShift;
+        by += v & kBinByMask;
+      }
+      if (pk) {
+        c.cnt[2 * f] += pk;
+        c.cnt[2 * f + 1] += by;
+      }
+    }
+  } else if (mode == 1) {
+    const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);
+    const uint32_t S = g2 / nb;
+    const uint64_t row = (uint64_t)nb * kBucket;
+    for (uint64_t f = t0; f < nflows; f += stride) {
+      uint64_t pk = 0, by = 0;
+      for (uint32_t s = 0; s < S; ++s) {
+        pk += c.lpart[2 * (s * row + f)];
+        by += c.lpart[2 * (s * row + f) + 1];
+      }
+      if (pk) {
+        const uint32_t id = c.cmap[f];
+        c.cnt[2ull * id] += pk;
+        c.cnt[2ull * id + 1] += by;
       }
     }
   }
 }
 
-// K3b: cnt[flow] += sum over K3 blocks of their packed partial bins.
-__global__ void k_count_reduce(CountArgs c, uint32_t nblocks) {
-  const uint64_t nflows = c.batch->flow_total;
-  if (nflows > (uint64_t)kCountBins) return;  // K3 used global atomics
-  for (uint64_t f = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; f < nflows;
-       f += (uint64_t)gridDim.x * blockDim.x) {
-    // 8 independent rows per step: the loads of a thread are in flight together
-    uint64_t pk = 0, by = 0;
-    uint32_t b = 0;
-    for (; b + 8 <= nblocks; b += 8) {
-      uint64_t v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = c.part[(uint64_t)(b + k) * kCountBins + f];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        pk += v[k] >> kBinPkShift;
-        by += v[k] & kBinByMask;
-      }
-    }
-    for (; b < nblocks; ++b) {
-      const uint64_t v = c.part[(uint64_t)b * kCountBins + f];
-      pk += v >> kBinPkShift;
-      by += v & kBinByMask;
-    }
-    if (pk) {
-      c.cnt[2 * f] += pk;
-      c.cnt[2 * f + 1] += by;
-    }
-  }
-}
 
 __global__ void k_finalize(BatchState* b, PersistState* p, uint64_t out_cap, uint64_t* out_n,
                            tcbee_counters* ctr, int direction) {
@@ -1167,8 +1392,9 @@ __global__ void k_merge_insert(MergeArgs g) {
     const uint64_t* E = g.ent + 8 * e;
     const uint64_t K[5] = {E[0], E[1], E[2], E[3], E[4]};
     uint64_t fs = ~0ull;
+    uint32_t claim;
     const uint32_t s = flow_upsert(g.tab, K, flow_hash64(K[0], K[1], K[2], K[3], K[4]), g.batch,
-                                   g.new_list, g.persist, fs);
+                                   g.new_list, g.persist, fs, claim);
     g.out_slot[e] = s;
     if (s == 0xFFFFFFFFu) continue;
     atomicAdd((unsigned long long*)&g.mcnt[2ull * s], (unsigned long long)E[5]);
@@ -1323,9 +1549,22 @@ hipError_t launch_rank(const RankArgs& r, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_count(const CountArgs& c, unsigned grid, hipStream_t s) {
-  hipLaunchKernelGGL(k_count, dim3(grid), dim3(kCountBlock), 0, s, c);
-  if (c.part) hipLaunchKernelGGL(k_count_reduce, dim3(kCountBins / 256), dim3(256), 0, s, c, grid);
+hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g2, hipStream_t s, int k3v) {
+  const dim3 grid(g1);
+  // k3v (TCBEE_K3ABL at context creation): timing-only ablation / tiling A/B
+  switch (k3v) {
+    case 1: hipLaunchKernelGGL((k_count<8, 1>), dim3(grid), dim3(kCountBlock), 0, s, c); break;
+    case 2: hipLaunchKernelGGL((k_count<8, 2>), dim3(grid), dim3(kCountBlock), 0, s, c); break;
+    case 4: hipLaunchKernelGGL((k_count<8, 4>), dim3(grid), dim3(kCountBlock), 0, s, c); break;
+    case 7: hipLaunchKernelGGL((k_count<8, 7>), dim3(grid), dim3(kCountBlock), 0, s, c); break;
+    case 16: hipLaunchKernelGGL((k_count<16, 0>), dim3(grid), dim3(kCountBlock), 0, s, c); break;
+    case 32: hipLaunchKernelGGL((k_count<4, 0>), dim3(grid), dim3(kCountBlock), 0, s, c); break;
+    default: hipLaunchKernelGGL((k_count<8, 0>), dim3(grid), dim3(kCountBlock), 0, s, c); break;
+  }
+  if (g2) hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1);
+  // mode 0 needs kCountBins threads; mode 1 up to nb_max * kBucket (grid-stride)
+  const unsigned gr = g2 ? 1024u : (unsigned)(kCountBins / 256);
+  hipLaunchKernelGGL(k_count_reduce, dim3(gr), dim3(256), 0, s, c, g1, g2);
   return hipGetLastError();
 }
 

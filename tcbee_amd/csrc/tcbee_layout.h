@@ -46,7 +46,8 @@ constexpr uint64_t kTagEmpty = 0, kTagBusy = 1;
 // ---- tcbee flow hash v1 (DESIGN.md "Flow hash") ---------------------------
 // 40-byte key read as 5 little-endian u64 words k[0..4]:
 //   h = 0x7CBEE; for each word: h ^= k*C1; h = rotl(h,31)*C2;  h = fmix64(h ^ 40)
-// flow_hash32 = lo32(h) ^ hi32(h); table tag = h (bumped to >= 2).
+// flow_hash32 = lo32(h) ^ hi32(h); table tag = hi32(h) (bumped to >= 2), kept in
+// the low half of a slot's tag word (the high half holds the flow's claim index).
 TCBEE_HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
 TCBEE_HD uint64_t fmix64(uint64_t k) {
   k ^= k >> 33;
@@ -67,7 +68,10 @@ TCBEE_HD uint64_t flow_hash64(uint64_t k0, uint64_t k1, uint64_t k2, uint64_t k3
   return fmix64(h ^ 40u);
 }
 TCBEE_HD uint32_t fold32(uint64_t h) { return (uint32_t)(h ^ (h >> 32)); }
-TCBEE_HD uint64_t hash_tag(uint64_t h) { return h < 2 ? h + 2 : h; }
+TCBEE_HD uint32_t hash_tag32(uint64_t h) {
+  const uint32_t t = (uint32_t)(h >> 32);
+  return t < 2 ? t + 2 : t;
+}
 
 // counter-based RNG for the synthetic generator (splitmix64)
 TCBEE_HD uint64_t splitmix64(uint64_t x) {

@@ -198,16 +198,44 @@ def test_lookback_recount_fallback(gpu, oracle, every, monkeypatch):
         assert p.status() == 0
 
 
-@pytest.mark.parametrize("budget,n,flows", [("64", 200_000, 300), ("1", 100_000, 3),
-                                            ("700", 400_000, 5000)])
-def test_k3_wave_flush_path(gpu, oracle, budget, n, flows, monkeypatch):
-    """K3's wave-local LDS-bin flush (atomic exchange under concurrent adds) forced
-    on every iteration: per-flow pkts/bytes stay exact."""
+@pytest.mark.parametrize("mode", ["bucket", "atomic"])
+@pytest.mark.parametrize("n,flows", [(300_000, 30_000), (200_000, 13_000), (120_000, 100_000)])
+def test_k3_large_table_modes(gpu, oracle, mode, n, flows, monkeypatch):
+    """More flows than K3's LDS bins (12288): mode 1 (claims bucketed per block,
+    per-bucket LDS histograms, claim->id in the reduce) and mode 2 (device atomics,
+    TCBEE_TEST_K3_NOBUCKET) both exact, over two batches (claims of batch 1 looked
+    up again in batch 2)."""
     from tracegen import mixed_trace
-    monkeypatch.setenv("TCBEE_TEST_K3_BUDGET", budget)
-    tr = mixed_trace(n, seed=93, n_flows=flows)
-    with tcbee_amd.PacketParser(max_frames=1 << 19, max_arena=1 << 27, max_flows=1 << 14) as p:
-        assert_same(p.parse(tr), oracle.parse(tr), p.flows())
+    if mode == "atomic":
+        monkeypatch.setenv("TCBEE_TEST_K3_NOBUCKET", "1")
+    tr = mixed_trace(n, seed=97, n_flows=flows)
+    cut = n // 3
+    with tcbee_amd.PacketParser(max_frames=1 << 19, max_arena=1 << 28, max_flows=1 << 18) as p:
+        r1 = p.parse(tr.slice(0, cut))
+        r2 = p.parse(tr.slice(cut, n))
+        rec, fh, fi, ctr, table = oracle.parse(tr)
+        assert np.array_equal(np.concatenate([r1.records, r2.records]), rec)
+        assert np.array_equal(np.concatenate([r1.flow_id, r2.flow_id]), fi)
+        fl = p.flows()
+        assert len(fl) == len(table) and np.array_equal(fl, table)
+        assert p.status() == 0
+
+
+@pytest.mark.parametrize("flows", [1, 40, 5000, 20_000])
+def test_k3_big_caplen_and_hot_flow(gpu, oracle, flows):
+    """caplen >= 64 KiB (counted by device atomics, outside the 40-bit LDS byte
+    field) mixed with ordinary frames, and one hot flow (the wave-uniform add)."""
+    from tracegen import mixed_trace
+    tr = mixed_trace(150_000, seed=101, n_flows=flows)
+    rng = np.random.default_rng(5)
+    big = rng.choice(tr.n, size=300, replace=False)
+    pad = 300_000
+    arena = np.concatenate([tr.arena, np.zeros(pad, np.uint8)])
+    ln = tr.caplen.copy()
+    ln[big] = rng.integers(65_536, pad, size=len(big)).astype(np.uint32)
+    tr2 = Trace(arena, tr.offset, ln, tr.ts_ns)
+    with tcbee_amd.PacketParser(max_frames=1 << 18, max_arena=1 << 27, max_flows=1 << 16) as p:
+        assert_same(p.parse(tr2), oracle.parse(tr2), p.flows())
         assert p.status() == 0
 
 

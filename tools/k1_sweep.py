@@ -24,8 +24,9 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--fpl", default="1,2,4")
     ap.add_argument("--workloads", default="imix10k,imix1,64B1")
-    ap.add_argument("--var", default="", help="extra env A/B, e.g. TCBEE_K3_ATOMIC=0,1")
+    ap.add_argument("--var", default="", help="extra env A/B, e.g. TCBEE_K3ABL=0,2")
     ap.add_argument("--flows-only", action="store_true", help="only the flows-on variants")
+    ap.add_argument("--cap-mult", type=float, default=4.0, help="max_flows = mult x flows")
     args = ap.parse_args()
     import torch
     import tcbee_amd
@@ -58,7 +59,7 @@ def main():
             if var_name:
                 os.environ[var_name] = vv
             parsers[(fpl, flows, vv)] = tcbee_amd.PacketParser(max_frames=n,
-                                                               max_flows=max(4 * nf, 4096))
+                                                               max_flows=max(int(args.cap_mult * nf), 4096))
         times = {v: [] for v in variants}
         k1 = {v: [] for v in variants}
         for r in range(args.rounds):
