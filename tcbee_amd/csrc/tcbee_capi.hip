@@ -23,7 +23,8 @@ struct tcbee_ctx {
   uint32_t withhold_every = 0;  // TCBEE_TEST_WITHHOLD (look-back recount test hook)
   int k3_no_bucket = 0;         // TCBEE_TEST_K3_NOBUCKET=1: large tables use K3 mode 2 (test hook)
   int k3_variant = 0;
-  uint32_t plain_walk = kPlainWalk;  // TCBEE_WALK: K1 plain probe walk length (A/B)           // TCBEE_K3ABL: timing-only K3 ablations / tilings (A/B)
+  uint32_t plain_walk = kPlainWalk;  // TCBEE_WALK: K1 plain probe walk length (A/B)
+  uint32_t pack_bits = 0;            // K1->K3 scratch packing (0: two words per record)           // TCBEE_K3ABL: timing-only K3 ablations / tilings (A/B)
 
   FlowTable tab{};
   uint64_t nslots = 0;
@@ -217,6 +218,14 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   c->nslots = 64;
   while (c->nslots < 2 * c->max_flows) c->nslots <<= 1;
   c->tab.mask = c->nslots - 1;
+  {
+    // claims < nslots: log2(nslots) bits + 1 (so no packed word is all ones, the
+    // no-flow mark); packed while at least 14 bits (caplen < 16383) remain
+    uint32_t b = 1;
+    while ((1ull << (b - 1)) < c->nslots) ++b;
+    c->pack_bits = b <= 18 ? b : 0;
+    if (const char* e = std::getenv("TCBEE_TEST_NOPACK")) c->pack_bits = std::atoi(e) ? 0 : c->pack_bits;
+  }
   c->max_tiles = (max_frames + tile_frames(1) - 1) / tile_frames(1);
   c->max_words = (max_frames + 31) / 32;
   c->max_sblocks = (c->max_words + kScanWordsPerBlock - 1) / kScanWordsPerBlock;
@@ -352,6 +361,7 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     a.filter_port = cfg->filter_port;
     a.withhold_every = c->withhold_every;
     a.plain_walk = c->plain_walk;
+    a.pack_bits = c->pack_bits;
     const bool timed = c->profiling && c->ev_used < kMaxProfiled;
     if (timed) TRY_HIP(hipEventRecord(c->ev[2 * c->ev_used], s));
     TRY_HIP(launch_parse(a, fpl, flows, s));
@@ -378,6 +388,7 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     k.direction = cfg->direction;
     k.persist_rw = c->d_persist;
     k.acc_flow = c->d_slot_scratch;
+    k.pack_bits = c->pack_bits;
     k.acc_len = c->d_len_scratch;
     k.out_id = out_flow_id;
     k.out_cap = out_cap;

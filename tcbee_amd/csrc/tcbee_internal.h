@@ -78,6 +78,7 @@ struct ParseArgs {
   uint16_t filter_port;
   uint32_t withhold_every;  // test hook (TCBEE_TEST_WITHHOLD): 0 in production
   uint32_t plain_walk;      // probe steps past foreign slots with plain loads (kPlainWalk)
+  uint32_t pack_bits;       // != 0: acc_flow = claim | min(caplen, lmax) << pack_bits
 };
 constexpr uint32_t kPlainWalk = 8;
 
@@ -103,6 +104,7 @@ struct CountArgs {
   int direction;
   PersistState* persist_rw;
   const uint32_t* acc_flow;
+  uint32_t pack_bits;        // as ParseArgs::pack_bits
   const uint32_t* acc_len;
   uint32_t* out_id;
   uint64_t out_cap;

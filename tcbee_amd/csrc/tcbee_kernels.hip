@@ -749,8 +749,18 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
     if (acc[f] && !(ABL & 16)) {
       if (a.out_hash && p < a.out_cap) st_stream<NT>(a.out_hash + p, hsh[f]);
       if (FLOWS) {
-        st_stream<NT>(a.acc_flow + p, claim[f]);
-        st_stream<NT>(a.acc_len + p, clen[f]);
+        if (a.pack_bits) {
+          // (claim, caplen) in one word; a caplen that does not fit saturates the
+          // field and is stored in full beside it (K3 reads it only then)
+          const uint32_t lmax = 0xFFFFFFFFu >> a.pack_bits;
+          const uint32_t lq = clen[f] < lmax ? clen[f] : lmax;
+          st_stream<NT>(a.acc_flow + p, claim[f] == 0xFFFFFFFFu ? 0xFFFFFFFFu
+                                                                : claim[f] | (lq << a.pack_bits));
+          if (lq == lmax) a.acc_len[p] = clen[f];
+        } else {
+          st_stream<NT>(a.acc_flow + p, claim[f]);
+          st_stream<NT>(a.acc_len + p, clen[f]);
+        }
       }
     }
     if (FLOWS) {
@@ -1020,6 +1030,45 @@ __device__ __forceinline__ uint64_t count_per(uint64_t n_acc, uint32_t grid) {
   return ((n_acc + grid - 1) / grid + kK3Gran - 1) / kK3Gran * kK3Gran;
 }
 
+// K1's per-record scratch of U accepted records p0 + k*kCountBlock (p < hi;
+// others give claim ~0, len 0): claim (~0: no flow) and caplen, packed in one
+// word when the context's table is small enough (pack_bits != 0). All words are
+// loaded before any is inspected (a branch between them would serialize them).
+template <int U, bool PACK>
+__device__ __forceinline__ void load_acc(const CountArgs& c, uint64_t p0, uint64_t lo, uint64_t hi,
+                                         uint32_t (&claim)[U], uint32_t (&len)[U]) {
+  uint32_t v[U];
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    const uint64_t p = p0 + (uint64_t)k * kCountBlock;
+    v[k] = __builtin_nontemporal_load(&c.acc_flow[p < hi ? p : lo]);
+    if (!PACK) len[k] = __builtin_nontemporal_load(&c.acc_len[p < hi ? p : lo]);
+  }
+  const uint32_t lmax = 0xFFFFFFFFu >> c.pack_bits;
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    const uint64_t p = p0 + (uint64_t)k * kCountBlock;
+    if (PACK) {
+      claim[k] = v[k] == 0xFFFFFFFFu ? v[k] : (v[k] & ((1u << c.pack_bits) - 1u));
+      len[k] = v[k] >> c.pack_bits;
+    } else {
+      claim[k] = v[k];
+    }
+    if (p >= hi) claim[k] = 0xFFFFFFFFu, len[k] = 0;
+  }
+  if (PACK) {
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      if (len[k] == lmax && claim[k] != 0xFFFFFFFFu) len[k] = c.acc_len[p0 + (uint64_t)k * kCountBlock];
+  }
+}
+
+template <bool PACK>
+__device__ __forceinline__ uint32_t load_claim(const CountArgs& c, uint64_t p) {
+  const uint32_t v = __builtin_nontemporal_load(&c.acc_flow[p]);
+  return (PACK && v != 0xFFFFFFFFu) ? (v & ((1u << c.pack_bits) - 1u)) : v;
+}
+
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -1050,7 +1099,7 @@ __device__ __forceinline__ uint32_t block1024_excl_scan(uint32_t v, uint32_t* s_
 }
 
 // Mode 1, phase 1 (inside k_count): ids out, bucket counts, scan, scatter.
-template <int U>
+template <int U, bool PACK>
 __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint64_t nflows,
                               uint32_t* hist, uint32_t* cur, uint32_t* s_w) {
   const uint32_t tid = threadIdx.x;
@@ -1062,7 +1111,7 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
-      s[k] = __builtin_nontemporal_load(&c.acc_flow[p < hi ? p : lo]);
+      s[k] = load_claim<PACK>(c, p < hi ? p : lo);
       if (p >= hi) s[k] = 0xFFFFFFFFu;
     }
     uint32_t id[U];
@@ -1092,14 +1141,7 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
   __syncthreads();
   for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
     uint32_t s[U], len[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
-      const uint64_t pc = p < hi ? p : lo;
-      s[k] = __builtin_nontemporal_load(&c.acc_flow[pc]);
-      len[k] = __builtin_nontemporal_load(&c.acc_len[pc]);
-      if (p >= hi) s[k] = 0xFFFFFFFFu;
-    }
+    load_acc<U, PACK>(c, base + tid, lo, hi, s, len);
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       if (s[k] != 0xFFFFFFFFu) {
@@ -1112,7 +1154,7 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
 
 // ABL3 (timing-only ablations, 0 in every product launch): 1 no bin updates,
 // 2 no id gather, 4 no id stores
-template <int U, int ABL3>
+template <int U, int ABL3, bool PACK>
 __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   __shared__ uint64_t s_bin[kCountBins];
   __shared__ uint32_t s_map[kCountBins];  // claim index -> dense id
@@ -1139,7 +1181,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
   if (mode == 1) {
     uint32_t* h = reinterpret_cast<uint32_t*>(s_bin);
-    count_scatter<U>(c, lo, hi, nflows, h, h + kMaxBuckets, s_w);
+    count_scatter<U, PACK>(c, lo, hi, nflows, h, h + kMaxBuckets, s_w);
     return;
   }
   if (mode == 0) {
@@ -1155,15 +1197,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   };
   for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
     uint32_t s[U], len[U], id[U];
-    // streamed once: non-temporal
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
-      const uint64_t pc = p < hi ? p : lo;  // unconditional loads
-      s[k] = __builtin_nontemporal_load(&c.acc_flow[pc]);
-      len[k] = __builtin_nontemporal_load(&c.acc_len[pc]);
-      if (p >= hi) s[k] = 0xFFFFFFFFu, len[k] = 0;
-    }
+    load_acc<U, PACK>(c, base + tid, lo, hi, s, len);  // streamed once: non-temporal
     if (ABL3 & 2) {
 #pragma unroll
       for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : (s[k] & 8191u);
@@ -1552,15 +1586,21 @@ hipError_t launch_rank(const RankArgs& r, hipStream_t s) {
 hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g2, hipStream_t s, int k3v) {
   const dim3 grid(g1);
   // k3v (TCBEE_K3ABL at context creation): timing-only ablation / tiling A/B
+#define KC(U, A)                                                                     \
+  do {                                                                               \
+    if (c.pack_bits) hipLaunchKernelGGL((k_count<U, A, true>), grid, dim3(kCountBlock), 0, s, c); \
+    else hipLaunchKernelGGL((k_count<U, A, false>), grid, dim3(kCountBlock), 0, s, c);            \
+  } while (0)
   switch (k3v) {
-    case 1: hipLaunchKernelGGL((k_count<8, 1>), dim3(grid), dim3(kCountBlock), 0, s, c); break;
-    case 2: hipLaunchKernelGGL((k_count<8, 2>), dim3(grid), dim3(kCountBlock), 0, s, c); break;
-    case 4: hipLaunchKernelGGL((k_count<8, 4>), dim3(grid), dim3(kCountBlock), 0, s, c); break;
-    case 7: hipLaunchKernelGGL((k_count<8, 7>), dim3(grid), dim3(kCountBlock), 0, s, c); break;
-    case 16: hipLaunchKernelGGL((k_count<16, 0>), dim3(grid), dim3(kCountBlock), 0, s, c); break;
-    case 32: hipLaunchKernelGGL((k_count<4, 0>), dim3(grid), dim3(kCountBlock), 0, s, c); break;
-    default: hipLaunchKernelGGL((k_count<8, 0>), dim3(grid), dim3(kCountBlock), 0, s, c); break;
+    case 1: KC(8, 1); break;
+    case 2: KC(8, 2); break;
+    case 4: KC(8, 4); break;
+    case 7: KC(8, 7); break;
+    case 16: KC(16, 0); break;
+    case 32: KC(4, 0); break;
+    default: KC(8, 0); break;
   }
+#undef KC
   if (g2) hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1);
   // mode 0 needs kCountBins threads; mode 1 up to nb_max * kBucket (grid-stride)
   const unsigned gr = g2 ? 1024u : (unsigned)(kCountBins / 256);

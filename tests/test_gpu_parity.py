@@ -221,18 +221,22 @@ def test_k3_large_table_modes(gpu, oracle, mode, n, flows, monkeypatch):
         assert p.status() == 0
 
 
+@pytest.mark.parametrize("nopack", ["0", "1"])
 @pytest.mark.parametrize("flows", [1, 40, 5000, 20_000])
-def test_k3_big_caplen_and_hot_flow(gpu, oracle, flows):
+def test_k3_big_caplen_and_hot_flow(gpu, oracle, flows, nopack, monkeypatch):
     """caplen >= 64 KiB (counted by device atomics, outside the 40-bit LDS byte
-    field) mixed with ordinary frames, and one hot flow (the wave-uniform add)."""
+    field) mixed with ordinary frames, and one hot flow (the wave-uniform add);
+    K1->K3 scratch packed (claim + 14-bit caplen, escapes stored beside) or not."""
     from tracegen import mixed_trace
+    monkeypatch.setenv("TCBEE_TEST_NOPACK", nopack)
     tr = mixed_trace(150_000, seed=101, n_flows=flows)
     rng = np.random.default_rng(5)
     big = rng.choice(tr.n, size=300, replace=False)
     pad = 300_000
     arena = np.concatenate([tr.arena, np.zeros(pad, np.uint8)])
     ln = tr.caplen.copy()
-    ln[big] = rng.integers(65_536, pad, size=len(big)).astype(np.uint32)
+    # 16383+ overflows the packed K1->K3 caplen field; 65536+ leaves the LDS bins
+    ln[big] = rng.integers(16_000, pad, size=len(big)).astype(np.uint32)
     tr2 = Trace(arena, tr.offset, ln, tr.ts_ns)
     with tcbee_amd.PacketParser(max_frames=1 << 18, max_arena=1 << 27, max_flows=1 << 16) as p:
         assert_same(p.parse(tr2), oracle.parse(tr2), p.flows())
