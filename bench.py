@@ -295,6 +295,15 @@ def main():
             out["config2_1M_64B"] = {"mpkts": round(1_000_000 * max(args.steps, 20) / e_el / 1e6, 1),
                                      "ms_per_step": round(e_el / max(args.steps, 20) * 1e3, 4),
                                      "k1_ms": round(e_k1, 4), "check": e_chk}
+            # one GPU's shard of config 4 (1B frames / 8 GPUs, 1M flows): every flow
+            # appears in every contiguous shard, so each GPU's table holds all 1M
+            c4_n, c4_steps = 125_000_000, 5
+            c_el, c_k1, c_n, c_chk = run_device(torch, None, 0, 1, c4_n, "imix", 1, 1_000_000,
+                                                c4_steps, 1, args.seed)
+            out["config4_shard_1M_flows"] = {
+                "frames": c4_n, "flows": 1_000_000, "mpkts": round(c4_n * c4_steps / c_el / 1e6, 1),
+                "ms_per_step": round(c_el / c4_steps * 1e3, 4), "k1_ms": round(c_k1, 4),
+                "check": c_chk}
             out["e2e_host"] = host_e2e(args.sizes, kind, args.flows, args.seed,
                                        n=args.e2e_frames)
         if not args.no_cpu and world == 1:

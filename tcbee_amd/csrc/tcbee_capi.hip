@@ -23,6 +23,7 @@ struct tcbee_ctx {
   uint32_t withhold_every = 0;  // TCBEE_TEST_WITHHOLD (look-back recount test hook)
   int k3_no_bucket = 0;         // TCBEE_TEST_K3_NOBUCKET=1: large tables use K3 mode 2 (test hook)
   int k3_variant = 0;
+  int k1_variant = 0;           // TCBEE_K1V: K1 staging/occupancy A/B variants
   uint32_t plain_walk = kPlainWalk;  // TCBEE_WALK: K1 plain probe walk length (A/B)
   uint32_t pack_bits = 0;            // K1->K3 scratch packing (0: two words per record)           // TCBEE_K3ABL: timing-only K3 ablations / tilings (A/B)
 
@@ -202,6 +203,7 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   if (const char* e = std::getenv("TCBEE_TEST_WITHHOLD")) c->withhold_every = (uint32_t)std::atoi(e);
   if (const char* e = std::getenv("TCBEE_TEST_K3_NOBUCKET")) c->k3_no_bucket = std::atoi(e);
   if (const char* e = std::getenv("TCBEE_K3ABL")) c->k3_variant = std::atoi(e);
+  if (const char* e = std::getenv("TCBEE_K1V")) c->k1_variant = std::atoi(e);
   if (const char* e = std::getenv("TCBEE_WALK")) c->plain_walk = (uint32_t)std::atoi(e);
   if (const char* e = std::getenv("TCBEE_FPL")) {
     const int v = std::atoi(e);
@@ -364,7 +366,7 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     a.pack_bits = c->pack_bits;
     const bool timed = c->profiling && c->ev_used < kMaxProfiled;
     if (timed) TRY_HIP(hipEventRecord(c->ev[2 * c->ev_used], s));
-    TRY_HIP(launch_parse(a, fpl, flows, s));
+    TRY_HIP(launch_parse(a, fpl, flows, s, c->k1_variant));
     if (timed) {
       TRY_HIP(hipEventRecord(c->ev[2 * c->ev_used + 1], s));
       ++c->ev_used;

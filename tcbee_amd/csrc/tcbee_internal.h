@@ -96,7 +96,7 @@ struct RankArgs {
 
 // Launchers (tcbee_kernels.hip). All asynchronous on `s`.
 hipError_t launch_table_init(FlowTable t, hipStream_t s);
-hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s);
+hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s, int k1v = 0);
 hipError_t launch_rank(const RankArgs& r, hipStream_t s);
 struct CountArgs {
   uint64_t* out_n;           // finalize (block 0): record count, counters, running bases

@@ -515,8 +515,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 // STAGE 0: the whole tile's records staged in LDS, stored by the block after the
 // look-back; STAGE 1: each wave stages and stores its own 64-record group per
 // round (its records are contiguous in the output), 4.7 KB of LDS per wave.
-template <int FPL, bool FLOWS, int PROBE_AUX, int ABL = 0, int STAGE = 0, bool NT = false>
-__global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
+// OCC: minimum waves per SIMD requested from the register allocator (0: default)
+template <int FPL, bool FLOWS, int PROBE_AUX, int ABL = 0, int STAGE = 0, bool NT = false, int OCC = 0>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, OCC ? 8 : 8)))
+void k_parse(ParseArgs a) {
   constexpr int TILE = kBlock * FPL;
   constexpr int WBUF_DW = (64 * kRecBytes + 32) / 4;
   constexpr int SREC_DW = STAGE ? 4 * WBUF_DW : (TILE * kRecBytes + 32) / 4;
@@ -1503,8 +1505,19 @@ hipError_t launch_table_init(FlowTable t, hipStream_t s) {
 }
 
 template <int FPL>
-static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s) {
+static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s, int k1v) {
   const dim3 grid((unsigned)a.ntiles);
+  // k1v (TCBEE_K1V at context creation): staging / occupancy A/B variants
+  if (FPL == 2 && flows && k1v) {
+    switch (k1v) {
+      case 1: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 0>), grid, dim3(kBlock), 0, s, a); break;
+      case 2: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 5>), grid, dim3(kBlock), 0, s, a); break;
+      case 3: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 6>), grid, dim3(kBlock), 0, s, a); break;
+      case 4: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 0, false, 5>), grid, dim3(kBlock), 0, s, a); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   // probe-load cache policy: plain (L1/L2-allocating) by default; TCBEE_PROBE_AUX=16
   // selects sc1 (agent-coherent, bypasses L1) for A/B runs
   static const int aux = [] {
@@ -1555,11 +1568,11 @@ static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s
   return hipGetLastError();
 }
 
-hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s) {
+hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s, int k1v) {
   switch (fpl) {
-    case 1: return launch_parse_fpl<1>(a, flows, s);
-    case 2: return launch_parse_fpl<2>(a, flows, s);
-    case 4: return launch_parse_fpl<4>(a, flows, s);
+    case 1: return launch_parse_fpl<1>(a, flows, s, k1v);
+    case 2: return launch_parse_fpl<2>(a, flows, s, k1v);
+    case 4: return launch_parse_fpl<4>(a, flows, s, k1v);
     default: return hipErrorInvalidValue;
   }
 }
