@@ -10,7 +10,9 @@ counters. Each step is one fresh trace (the flow table starts empty). With
 --gpus N each rank parses its own contiguous shard of one global trace (weak
 scaling, no frame exchange); per step the compact per-rank flow tables are
 all-gathered over RCCL, merged on every GPU (global dense first-seen ids) and
-each rank's record flow ids are remapped; the counters are all-reduced.
+each rank's record flow ids are remapped; the counters are all-reduced. That
+exchange runs on a side stream and overlaps the next step's parse (two output
+slots; tcbee_amd.dist.OverlappedMerge); the timed region ends after all of it.
 
 Prints ONE JSON line (rank 0). See DESIGN.md "Measurement".
 """
@@ -53,49 +55,69 @@ def build_device_trace(torch, n, sizes, kind, n_flows, seed, first_index, stream
     return d_arena, alen, d_off, d_len, d_ts
 
 
-def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup, seed):
+def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup, seed,
+               multi=None):
     import tcbee_amd
     stream = torch.cuda.current_stream().cuda_stream
+    # multi: the N>1 exchange runs (also at N=1 under TCBEE_BENCH_FORCE_MERGE=1, a
+    # one-GPU rehearsal of its cost and of the overlap)
+    multi = world > 1 if multi is None else multi
     first = rank * n
     d_arena, alen, d_off, d_len, d_ts = build_device_trace(torch, n, sizes, kind, n_flows,
                                                            seed, first, stream)
-    d_rec = torch.empty(n * 74 + 64, dtype=torch.uint8, device="cuda")
-    d_hash = torch.empty(n, dtype=torch.int32, device="cuda")
-    d_id = torch.empty(n, dtype=torch.int32, device="cuda")
-    d_n = torch.zeros(1, dtype=torch.int64, device="cuda")
-    d_ctr = torch.zeros(4, dtype=torch.int64, device="cuda")
+    # N>1: two output slots, so that step i's flow-table exchange (side stream) overlaps
+    # step i+1's parse (main stream)
+    overlap = multi and os.environ.get("TCBEE_BENCH_OVERLAP", "1") != "0"
+    nbuf = 2 if overlap else 1
+    slots = [{"rec": torch.empty(n * 74 + 64, dtype=torch.uint8, device="cuda"),
+              "hash": torch.empty(n, dtype=torch.int32, device="cuda"),
+              "id": torch.empty(n, dtype=torch.int32, device="cuda"),
+              "n": torch.zeros(1, dtype=torch.int64, device="cuda"),
+              "ctr": torch.zeros(4, dtype=torch.int64, device="cuda")} for _ in range(nbuf)]
     cap = max(4 * n_flows, 1 << 12)
     p = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=n, max_arena=0,
                                max_flows=cap)
-    merged = fm = None
-    if world > 1:
-        from tcbee_amd.dist import FlowMerge
+    merged = om = fm = None
+    if multi:
+        from tcbee_amd.dist import FlowMerge, OverlappedMerge
         merged = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=1024,
                                         max_arena=0, max_flows=world * cap)
-        fm = FlowMerge(p, merged, cap, world * n)
+        fm = FlowMerge(p, merged, cap, world * n, nbuf=nbuf)
+        om = OverlappedMerge(fm, nbuf=nbuf) if overlap else None
+    count = [0]
 
     def step():
         # one step = one fresh trace: empty flow table, parse + classify the shard,
-        # then (N>1) the RCCL flow-table merge and the local->global id remap
+        # then (N>1) the RCCL flow-table merge, the local->global id remap and the
+        # counter all-reduce, overlapping the next step's parse
+        k = count[0] % nbuf
+        count[0] += 1
+        b = slots[k]
+        if multi:
+            if om is not None:
+                om.acquire(k)
+            b["ctr"].zero_()
         p.reset_flows(stream=stream, sync=False)
-        p.parse_device(d_arena, alen, d_off, d_len, d_ts, n, d_rec, n, d_hash, d_id, d_n,
-                       d_ctr, stream=stream)
-        if world > 1:
-            fm.step(d_id, d_n, n, stream=stream)
-            dist.all_reduce(d_ctr)  # RCCL: global INGRESS/HANDLED/DROPPED
+        p.parse_device(d_arena, alen, d_off, d_len, d_ts, n, b["rec"], n, b["hash"], b["id"],
+                       b["n"], b["ctr"], stream=stream)
+        if om is not None:
+            om.submit(k, b["id"], b["n"], n, ctr=b["ctr"])
+        elif fm is not None:  # TCBEE_BENCH_OVERLAP=0: the exchange in line, one stream
+            fm.step(b["id"], b["n"], n, stream=stream)
+            dist.all_reduce(b["ctr"])
 
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     p.profile(True)
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if multi:
         dist.barrier()
     t1 = time.perf_counter()
     k1_ms, k1_launches = p.profile_read()
@@ -103,17 +125,20 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     status = p.status()
 
     # validation (untimed): counts, flow table, and a bit-exact sample vs the oracle
-    nrec = int(d_n.item())
+    last = slots[(count[0] - 1) % nbuf]
+    nrec = int(last["n"].item())
     flows = (merged if merged is not None else p).flows()
     check = {"records": nrec, "flows": int(len(flows)), "status": status,
              "pkts_total": int(flows["pkts"].sum())}
+    if multi:
+        check["ingress_global"] = int(last["ctr"][0].item())
     if rank == 0:
-        check.update(validate_sample(torch, d_rec, d_hash, n, sizes, kind, n_flows, seed,
-                                     first, nrec))
+        check.update(validate_sample(torch, last["rec"], last["hash"], n, sizes, kind, n_flows,
+                                     seed, first, nrec))
     p.close()
     if merged is not None:
         merged.close()
-    del d_arena, d_rec
+    del d_arena, slots
     torch.cuda.empty_cache()
     return elapsed, k1_ms / max(k1_launches, 1), nrec, check
 
@@ -240,7 +265,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    force_merge = os.environ.get("TCBEE_BENCH_FORCE_MERGE") == "1"
+    if world > 1 or force_merge:
         import torch.distributed as dist
         # one process per GPU; TCBEE_DIST_BACKEND=gloo + fewer GPUs than ranks only for
         # rehearsing the N>1 path on a 1-GPU box (ranks then share a device)
@@ -253,11 +279,16 @@ def main():
             dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
+    # One explicit stream for torch ops, RCCL and every tcbee call: the C ABI reads a
+    # NULL stream as "the context's own (non-blocking) stream", so passing torch's
+    # default-stream handle (0) would put the parse/merge on streams the collectives
+    # and the remap do not wait for.
+    torch.cuda.set_stream(torch.cuda.Stream())
     kind = 1 if args.flows > 1 else 0
 
     elapsed, k1_ms, nrec, check = run_device(torch, dist, rank, world, args.frames, args.sizes,
                                              kind, args.flows, args.steps, args.warmup,
-                                             args.seed)
+                                             args.seed, multi=world > 1 or force_merge)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -281,7 +312,8 @@ def main():
                                     f"{args.flows} flows" if args.sizes == "imix"
                                     else f"64B IPv4/TCP, {args.flows} flow(s)"),
                        "frames_per_gpu": args.frames, "flows": args.flows,
-                       "parallelism": f"shard{world}"},
+                       "parallelism": f"shard{world}" + ("+merge" if force_merge and world == 1
+                                                         else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          **pmc_traffic(args, k1_ms), "kernel": "k_parse",
@@ -318,7 +350,7 @@ def main():
                            "per-thread FLOWS(100) + bincode serialize"),
                 "single_thread": round(res[1][0], 2)}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
 

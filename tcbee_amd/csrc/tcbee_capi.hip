@@ -240,6 +240,9 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   if ((e = dalloc(&c->d_tile_status, c->max_tiles)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_new_list, c->nslots)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_bitmap, c->max_words)) != hipSuccess) return fail(map_err(e));
+  // all zero between batches from here on (K3 clears the words a batch set)
+  if ((e = hipMemset(c->d_bitmap, 0, c->max_words * sizeof(uint32_t))) != hipSuccess)
+    return fail(map_err(e));
   if ((e = dalloc(&c->d_wprefix, c->max_words)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_bprefix, c->max_sblocks)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_slot_scratch, max_frames)) != hipSuccess) return fail(map_err(e));
@@ -289,6 +292,8 @@ int tcbee_flow_reset(tcbee_ctx* c) {
   TRY_HIP(hipSetDevice(c->device));
   TRY_HIP(launch_table_init(c->tab, c->stream));
   TRY_HIP(hipMemsetAsync(c->d_persist, 0, sizeof(PersistState), c->stream));
+  // also the recovery point after a failed batch: the first-seen bitmap is whole-zero
+  TRY_HIP(hipMemsetAsync(c->d_bitmap, 0, c->max_words * sizeof(uint32_t), c->stream));
   TRY_HIP(hipStreamSynchronize(c->stream));
   c->reset_pending = false;
   return TCBEE_OK;
@@ -333,8 +338,6 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     pa.batch = c->d_batch;
     pa.tile_status = c->d_tile_status;
     pa.ntiles = ntiles;
-    pa.bitmap = c->d_bitmap;
-    pa.nwords = nwords;
     pa.reset = c->reset_pending;
     pa.tab = c->tab;
     pa.persist = c->d_persist;
@@ -397,6 +400,7 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     k.batch = c->d_batch;
     k.persist = c->d_persist;
     k.cmap = c->tab.cmap;
+    k.bitmap = c->d_bitmap;
     k.cnt = c->tab.cnt;
     k.part = c->d_count_part;
     k.region = c->d_k3_region;
@@ -542,6 +546,7 @@ int tcbee_flow_merge_device(tcbee_ctx* c, const tcbee_flow_entry* ent_dev, uint6
     c->d_mbprefix = nullptr;
     c->m_words = 0;
     TRY_HIP(dalloc(&c->d_mbitmap, words));
+    TRY_HIP(hipMemset(c->d_mbitmap, 0, words * sizeof(uint32_t)));  // cleared after each use
     TRY_HIP(dalloc(&c->d_mwprefix, words));
     TRY_HIP(dalloc(&c->d_mbprefix, (words + kScanWordsPerBlock - 1) / kScanWordsPerBlock));
     c->m_words = words;
@@ -552,7 +557,6 @@ int tcbee_flow_merge_device(tcbee_ctx* c, const tcbee_flow_entry* ent_dev, uint6
   TRY_HIP(hipMemsetAsync(c->d_persist, 0, sizeof(PersistState), s));
   TRY_HIP(hipMemsetAsync(c->d_batch, 0, sizeof(BatchState), s));
   TRY_HIP(hipMemsetAsync(c->d_mcnt, 0, 2 * c->nslots * sizeof(uint64_t), s));
-  TRY_HIP(hipMemsetAsync(c->d_mbitmap, 0, words * sizeof(uint32_t), s));
   MergeArgs g{};
   g.ent = reinterpret_cast<const uint64_t*>(ent_dev);
   g.nseg = nseg;
@@ -564,6 +568,7 @@ int tcbee_flow_merge_device(tcbee_ctx* c, const tcbee_flow_entry* ent_dev, uint6
   g.new_list = c->d_new_list;
   g.mcnt = c->d_mcnt;
   g.out_slot = out_ids_dev;
+  g.bitmap = c->d_mbitmap;
   RankArgs r{};
   r.new_list = c->d_new_list;
   r.batch = c->d_batch;

@@ -41,7 +41,8 @@ struct BatchState {
   uint64_t n_acc;       // accepted frames in this batch (last tile writes it)
   uint64_t n_new;       // flows first claimed in this batch
   uint64_t flow_total;  // flows with ids after this batch (rank step writes it)
-  uint64_t pad1;
+  uint64_t fs_max_word; // highest first-seen bitmap word set this batch (bounds the
+                        // rank scan; the words up to it are cleared again by K3)
 };
 static_assert(sizeof(BatchState) == 32, "memset size");
 
@@ -49,8 +50,6 @@ struct PrepArgs {
   BatchState* batch;
   uint64_t* tile_status;
   uint64_t ntiles;
-  uint32_t* bitmap;
-  uint64_t nwords;
   bool reset;           // also empty the flow table (a pending tcbee_flow_reset_device)
   FlowTable tab;
   PersistState* persist;
@@ -111,6 +110,7 @@ struct CountArgs {
   const BatchState* batch;
   const PersistState* persist;
   const uint32_t* cmap;      // claim index -> dense id
+  uint32_t* bitmap;          // first-seen bitmap: words [0, fs_max_word] cleared here
   uint64_t* cnt;
   uint64_t* part;            // mode 0: [g1][kCountBins] per-block packed bins
   // mode 1 (large tables; region == nullptr disables it)
@@ -132,6 +132,7 @@ struct MergeArgs {
   uint64_t* new_list;
   uint64_t* mcnt;             // per-slot pkts/bytes (2 * slots), zeroed
   uint32_t* out_slot;         // per entry: slot, then merged id
+  uint32_t* bitmap;           // merge first-seen bitmap (cleared after use)
 };
 hipError_t launch_export(FlowTable t, uint64_t* out, uint64_t cap, const PersistState* p,
                          uint64_t* n_out, hipStream_t s);

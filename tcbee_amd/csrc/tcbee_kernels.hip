@@ -809,7 +809,8 @@ __global__ void k_prep(PrepArgs p) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   if (t0 < 4) reinterpret_cast<uint64_t*>(p.batch)[t0] = 0;
   for (uint64_t i = t0; i < p.ntiles; i += stride) p.tile_status[i] = 0;
-  for (uint64_t i = t0; i < p.nwords; i += stride) p.bitmap[i] = 0;
+  // (the first-seen bitmap is not swept here: it is all zero between batches —
+  //  K3 clears the words the rank step set)
   if (p.reset) {
     if (t0 < sizeof(PersistState) / 8) reinterpret_cast<uint64_t*>(p.persist)[t0] = 0;
     const uint64_t nslots = p.tab.mask + 1;
@@ -863,16 +864,30 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
     }
     return;
   }
+  uint64_t wmax = 0;
   for (uint64_t j = tid; j < n_new; j += 1024) {
     const uint64_t local = r.tab.meta[8 * r.new_list[j] + 6] - base;
-    if ((local >> 5) < r.nwords) atomicOr(&r.bitmap[local >> 5], 1u << (local & 31));
+    if ((local >> 5) < r.nwords) {
+      atomicOr(&r.bitmap[local >> 5], 1u << (local & 31));
+      wmax = (local >> 5) > wmax ? (local >> 5) : wmax;
+    }
   }
+  // words past the last first-seen position are all zero: scan only [0, lim)
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t y = __shfl_xor(wmax, o);
+    wmax = y > wmax ? y : wmax;
+  }
+  __shared__ uint64_t s_wmax[16];
+  if (lane == 0) s_wmax[wave] = wmax;
   __syncthreads();
+  for (int w = 0; w < 16; ++w) wmax = s_wmax[w] > wmax ? s_wmax[w] : wmax;
+  if (tid == 0) r.batch->fs_max_word = wmax;
+  const uint64_t lim = wmax + 1 < r.nwords ? wmax + 1 : r.nwords;
   // wave w owns words [w*per, (w+1)*per), per a multiple of 64; lane l holds words
   // w*per + 64k + l in wv[k]. Wave totals first (for the wave's base), then a
   // per-64-word scan writes the exclusive prefixes.
   constexpr int kMaxK = (int)(kRankSmallWords / 1024);
-  const uint32_t per = (uint32_t)((r.nwords + 16 * 64 - 1) / (16 * 64)) * 64u;
+  const uint32_t per = (uint32_t)((lim + 16 * 64 - 1) / (16 * 64)) * 64u;
   const uint64_t w0 = (uint64_t)wave * per;
   const uint32_t kk = per / 64u;
   uint32_t wv[kMaxK];
@@ -880,7 +895,7 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
 #pragma unroll
   for (int k = 0; k < kMaxK; ++k) {
     const uint64_t w = w0 + 64u * k + lane;
-    wv[k] = ((uint32_t)k < kk && w < r.nwords)
+    wv[k] = ((uint32_t)k < kk && w < lim)
                 ? __hip_atomic_load(&r.bitmap[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                 : 0u;
     mine += __popc(wv[k]);
@@ -902,7 +917,7 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
         if (lane >= (uint32_t)o) x += y;
       }
       const uint64_t w = w0 + 64u * k + lane;
-      if (w < r.nwords) r.wprefix[w] = carry + x - c;
+      if (w < lim) r.wprefix[w] = carry + x - c;
       carry += __shfl(x, 63);
     }
   }
@@ -918,15 +933,37 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
   }
 }
 
-__global__ void k_mark(RankArgs r) {
+__global__ __launch_bounds__(kBlock) void k_mark(RankArgs r) {
+  __shared__ uint64_t s_wmax[kBlock / 64];
   const uint64_t n_new = r.batch->n_new;
   const uint64_t base = r.persist->rec_base;
+  uint64_t wmax = 0;
   for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n_new;
        j += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t s = r.new_list[j];
     const uint64_t local = r.tab.meta[8 * s + 6] - base;
-    if ((local >> 5) < r.nwords) atomicOr(&r.bitmap[local >> 5], 1u << (local & 31));
+    if ((local >> 5) < r.nwords) {
+      atomicOr(&r.bitmap[local >> 5], 1u << (local & 31));
+      wmax = (local >> 5) > wmax ? (local >> 5) : wmax;
+    }
   }
+  // highest word set (one device atomic per block): bounds the scan and the clear
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t y = __shfl_xor(wmax, o);
+    wmax = y > wmax ? y : wmax;
+  }
+  if ((threadIdx.x & 63u) == 0) s_wmax[threadIdx.x >> 6] = wmax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kBlock / 64; ++w) wmax = s_wmax[w] > wmax ? s_wmax[w] : wmax;
+    if (wmax) atomicMax((unsigned long long*)&r.batch->fs_max_word, (unsigned long long)wmax);
+  }
+}
+
+// words [0, lim) of the bitmap can be non-zero this batch
+__device__ __forceinline__ uint64_t rank_words(const RankArgs& r) {
+  const uint64_t m = r.batch->fs_max_word + 1;
+  return m < r.nwords ? m : r.nwords;
 }
 
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp, uint32_t& total) {
@@ -953,32 +990,37 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp,
 
 __global__ __launch_bounds__(kBlock) void k_scan_words(RankArgs r) {
   __shared__ uint32_t s_tmp[4];
-  const uint64_t w0 = (uint64_t)blockIdx.x * kScanWordsPerBlock + threadIdx.x * 8ull;
-  uint32_t c[8], sum = 0;
+  const uint64_t lim = rank_words(r);
+  // grid-stride over scan blocks (the launch covers the batch; only [0, lim) is live)
+  for (uint64_t b = blockIdx.x; b * kScanWordsPerBlock < lim; b += gridDim.x) {  // block-uniform
+    const uint64_t w0 = b * kScanWordsPerBlock + threadIdx.x * 8ull;
+    uint32_t c[8], sum = 0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    c[k] = (w0 + k < r.nwords) ? (uint32_t)__popc(r.bitmap[w0 + k]) : 0u;
-    sum += c[k];
-  }
-  uint32_t total;
-  uint32_t pre = block_excl_scan(sum, s_tmp, total);
+    for (int k = 0; k < 8; ++k) {
+      c[k] = (w0 + k < lim) ? (uint32_t)__popc(r.bitmap[w0 + k]) : 0u;
+      sum += c[k];
+    }
+    uint32_t total;
+    uint32_t pre = block_excl_scan(sum, s_tmp, total);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if (w0 + k < r.nwords) r.wprefix[w0 + k] = pre;
-    pre += c[k];
+    for (int k = 0; k < 8; ++k) {
+      if (w0 + k < lim) r.wprefix[w0 + k] = pre;
+      pre += c[k];
+    }
+    if (threadIdx.x == 0) r.bprefix[b] = total;
   }
-  if (threadIdx.x == 0) r.bprefix[blockIdx.x] = total;
 }
 
 __global__ __launch_bounds__(kBlock) void k_scan_blocks(RankArgs r) {
   __shared__ uint32_t s_tmp[4];
   uint32_t carry = 0;
-  for (uint64_t b0 = 0; b0 < r.nblocks; b0 += kBlock) {
+  const uint64_t nb = (rank_words(r) + kScanWordsPerBlock - 1) / kScanWordsPerBlock;
+  for (uint64_t b0 = 0; b0 < nb; b0 += kBlock) {
     const uint64_t b = b0 + threadIdx.x;
-    const uint32_t v = b < r.nblocks ? r.bprefix[b] : 0u;
+    const uint32_t v = b < nb ? r.bprefix[b] : 0u;
     uint32_t total;
     const uint32_t pre = block_excl_scan(v, s_tmp, total);
-    if (b < r.nblocks) r.bprefix[b] = carry + pre;
+    if (b < nb) r.bprefix[b] = carry + pre;
     carry += total;
   }
 }
@@ -1176,6 +1218,13 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
     }
     c.persist_rw->rec_base += n_acc;
     c.persist_rw->flow_count = nflows;
+  }
+  {
+    // the first-seen bitmap back to all-zero (the rank kernels are done with it)
+    const uint64_t wlast = c.batch->fs_max_word;
+    for (uint64_t w = blockIdx.x * (uint64_t)kCountBlock + tid; w <= wlast;
+         w += (uint64_t)gridDim.x * kCountBlock)
+      c.bitmap[w] = 0;
   }
   const int mode = count_mode(c, nflows);
   const uint64_t per = count_per(n_acc, gridDim.x);
@@ -1458,6 +1507,7 @@ __global__ void k_merge_finish(MergeArgs g) {
     g.tab.cnt[2 * id] = g.mcnt[2 * s];
     g.tab.cnt[2 * id + 1] = g.mcnt[2 * s + 1];
   }
+  for (uint64_t w = t0; w <= g.batch->fs_max_word; w += stride) g.bitmap[w] = 0;
   if (t0 == 0) {
     uint64_t recs = 0;
     for (uint64_t q = 0; q < g.nseg; ++q) recs += g.seg_meta[2 * q + 1];
@@ -1466,14 +1516,51 @@ __global__ void k_merge_finish(MergeArgs g) {
   }
 }
 
-__global__ void k_remap(uint32_t* ids, uint64_t n_max, const uint64_t* n_dev, const uint32_t* map,
-                        uint64_t map_len) {
+// ids[p] = map[ids[p]] (N>1 local -> global flow ids). The first kRemapLds map
+// entries are staged in LDS (a rank's local ids are dense from 0); the ids stream
+// through as 16-B non-temporal vectors, 4 per thread in flight.
+constexpr uint32_t kRemapLds = 16384;
+constexpr int kRemapBlock = 512;
+__global__ __launch_bounds__(kRemapBlock) void k_remap(uint32_t* ids, uint64_t n_max,
+                                                       const uint64_t* n_dev, const uint32_t* map,
+                                                       uint64_t map_len) {
+  __shared__ uint32_t s_map[kRemapLds];
   const uint64_t n = n_dev && *n_dev < n_max ? *n_dev : n_max;
-  for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < n;
-       p += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t v = ids[p];
-    ids[p] = v < map_len ? map[v] : 0xFFFFFFFFu;
+  const uint32_t m = map_len < kRemapLds ? (uint32_t)map_len : kRemapLds;
+  for (uint32_t j = threadIdx.x; j < m; j += kRemapBlock) s_map[j] = map[j];
+  __syncthreads();
+  auto tr = [&](uint32_t v) -> uint32_t {
+    return v < m ? s_map[v] : (v < map_len ? map[v] : 0xFFFFFFFFu);
+  };
+  const uint64_t t0 = blockIdx.x * (uint64_t)kRemapBlock + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * kRemapBlock;
+  uint64_t head = ((16u - ((uintptr_t)ids & 15u)) & 15u) >> 2;  // scalar up to 16-B alignment
+  if (head > n) head = n;
+  for (uint64_t p = t0; p < head; p += stride) ids[p] = tr(ids[p]);
+  u32x4* v4 = reinterpret_cast<u32x4*>(ids + head);
+  const uint64_t n4 = (n - head) >> 2;
+  constexpr int R = 4;
+  for (uint64_t q0 = t0; q0 < n4; q0 += stride * R) {
+    u32x4 v[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const uint64_t q = q0 + (uint64_t)u * stride;
+      v[u] = __builtin_nontemporal_load(v4 + (q < n4 ? q : n4 - 1));  // unconditional loads
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const uint64_t q = q0 + (uint64_t)u * stride;
+      if (q < n4) {
+        u32x4 o;
+        o[0] = tr(v[u][0]);
+        o[1] = tr(v[u][1]);
+        o[2] = tr(v[u][2]);
+        o[3] = tr(v[u][3]);
+        __builtin_nontemporal_store(o, v4 + q);
+      }
+    }
   }
+  for (uint64_t p = head + (n4 << 2) + t0; p < n; p += stride) ids[p] = tr(ids[p]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1508,12 +1595,11 @@ template <int FPL>
 static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s, int k1v) {
   const dim3 grid((unsigned)a.ntiles);
   // k1v (TCBEE_K1V at context creation): staging / occupancy A/B variants
-  if (FPL == 2 && flows && k1v) {
+  if constexpr (FPL == 2) if (flows && k1v) {
     switch (k1v) {
       case 1: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 0>), grid, dim3(kBlock), 0, s, a); break;
       case 2: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 5>), grid, dim3(kBlock), 0, s, a); break;
       case 3: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 6>), grid, dim3(kBlock), 0, s, a); break;
-      case 4: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 0, false, 5>), grid, dim3(kBlock), 0, s, a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1578,7 +1664,7 @@ hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s, 
 }
 
 hipError_t launch_prep(const PrepArgs& p, hipStream_t s) {
-  uint64_t work = p.ntiles > p.nwords ? p.ntiles : p.nwords;
+  uint64_t work = p.ntiles;
   if (p.reset && p.tab.mask + 1 > work) work = p.tab.mask + 1;
   hipLaunchKernelGGL(k_prep, dim3(grid_for(work < 4 ? 4 : work)), dim3(kBlock), 0, s, p);
   return hipGetLastError();
@@ -1590,7 +1676,8 @@ hipError_t launch_rank(const RankArgs& r, hipStream_t s) {
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_mark, dim3(1024), dim3(kBlock), 0, s, r);
-  hipLaunchKernelGGL(k_scan_words, dim3((unsigned)r.nblocks), dim3(kBlock), 0, s, r);
+  hipLaunchKernelGGL(k_scan_words, dim3((unsigned)(r.nblocks < 512 ? r.nblocks : 512)), dim3(kBlock),
+                     0, s, r);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, r);
   hipLaunchKernelGGL(k_assign, dim3(1024), dim3(kBlock), 0, s, r);
   return hipGetLastError();
@@ -1645,7 +1732,9 @@ hipError_t launch_merge(const MergeArgs& g, const RankArgs& r, hipStream_t s) {
 
 hipError_t launch_remap(uint32_t* ids, uint64_t n_max, const uint64_t* n_dev, const uint32_t* map,
                         uint64_t map_len, hipStream_t s) {
-  hipLaunchKernelGGL(k_remap, dim3(grid_for(n_max)), dim3(kBlock), 0, s, ids, n_max, n_dev, map,
+  const uint64_t want = (n_max + 4ull * kRemapBlock - 1) / (4ull * kRemapBlock);
+  hipLaunchKernelGGL(k_remap, dim3((unsigned)(want < 512 ? (want ? want : 1) : 512)),
+                     dim3(kRemapBlock), 0, s, ids, n_max, n_dev, map,
                      map_len);
   return hipGetLastError();
 }

@@ -55,21 +55,30 @@ class FlowMerge:
     then rewrite this rank's record flow ids from local to global ids."""
 
     def __init__(self, local: "_parser.PacketParser", merged: "_parser.PacketParser",
-                 cap: int, max_total_records: int, group=None):
+                 cap: int, max_total_records: int, group=None, nbuf: int = 1):
         self.local, self.merged, self.cap = local, merged, cap
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.max_total = max_total_records
         dev = torch.device("cuda", torch.cuda.current_device())
-        self.ent = torch.zeros((cap, ENTRY_WORDS), dtype=torch.int64, device=dev)
-        self.meta = torch.zeros(2, dtype=torch.int64, device=dev)
+        # nbuf export slots: a slot is read by the all-gather while the next step may
+        # already export into another one (OverlappedMerge)
+        self.ent = [torch.zeros((cap, ENTRY_WORDS), dtype=torch.int64, device=dev)
+                    for _ in range(nbuf)]
+        self.meta = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(nbuf)]
         self.ids = torch.empty(self.world * cap, dtype=torch.int32, device=dev)
 
-    def step(self, out_id: torch.Tensor | None, n_dev: torch.Tensor | None, n_max: int,
-             stream: int | None = None):
-        self.local.export_device(self.ent, self.cap, self.meta, stream=stream)
-        all_ent, all_meta = gather_tables(self.ent, self.meta, self.group)
+    def export(self, slot: int = 0, stream: int | None = None) -> None:
+        """Snapshot of the local table into export slot `slot` (before the next parse).
+        Pass a non-NULL stream handle: NULL means the context's own stream."""
+        self.local.export_device(self.ent[slot], self.cap, self.meta[slot], stream=stream)
+
+    def merge(self, slot: int, out_id: torch.Tensor | None, n_dev: torch.Tensor | None,
+              n_max: int, stream: int | None = None):
+        """All-gather slot's tables (RCCL, current torch stream), merge them on this GPU
+        and rewrite out_id from local to global ids, on `stream`."""
+        all_ent, all_meta = gather_tables(self.ent[slot], self.meta[slot], self.group)
         self.merged.merge_device(all_ent, self.world, self.cap, all_meta, self.max_total,
                                  self.ids, stream=stream)
         if out_id is not None:
@@ -77,3 +86,42 @@ class FlowMerge:
             _parser.remap_ids_device(out_id, n_max, n_dev, self.ids[lo:lo + self.cap],
                                      self.cap, stream=stream)
         return all_ent, all_meta
+
+    def step(self, out_id: torch.Tensor | None, n_dev: torch.Tensor | None, n_max: int,
+             stream: int | None = None):
+        """export + merge on one stream (the torch current stream must be `stream`)."""
+        self.export(0, stream=stream)
+        return self.merge(0, out_id, n_dev, n_max, stream=stream)
+
+
+class OverlappedMerge:
+    """Step i's exchange (all-gather, merge, id remap, counter all-reduce) runs on a
+    side stream and overlaps step i+1's parse on the main stream. Output buffers
+    rotate over `nbuf` slots; acquire(slot) makes the main stream wait until the
+    slot's previous exchange is done with them. Only the export (a snapshot of the
+    local table) stays on the main stream, ahead of the next step's table reset."""
+
+    def __init__(self, fm: FlowMerge, nbuf: int = 2):
+        assert len(fm.ent) >= nbuf
+        self.fm, self.nbuf = fm, nbuf
+        self.side = torch.cuda.Stream()
+        self.done = [None] * nbuf
+
+    def acquire(self, slot: int) -> None:
+        if self.done[slot] is not None:
+            torch.cuda.current_stream().wait_event(self.done[slot])
+
+    def submit(self, slot: int, out_id: torch.Tensor | None, n_dev: torch.Tensor | None,
+               n_max: int, ctr: torch.Tensor | None = None) -> None:
+        main = torch.cuda.current_stream()
+        self.fm.export(slot, stream=main.cuda_stream)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(ready)
+            self.fm.merge(slot, out_id, n_dev, n_max, stream=self.side.cuda_stream)
+            if ctr is not None:
+                dist.all_reduce(ctr, group=self.fm.group)  # global INGRESS/HANDLED/DROPPED
+            done = torch.cuda.Event()
+            done.record(self.side)
+        self.done[slot] = done

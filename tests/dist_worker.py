@@ -38,3 +38,65 @@ def run(rank, world, port, n, cap, result_dir):
              gids=gids, lo=lo, hi=hi, nrec=len(rec))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def run_gpu(rank, world, port, n, cap, result_dir, mode):
+    """N>1 choreography on the GPU: ranks share device 0 over gloo. mode "step":
+    FlowMerge.step on one stream; mode "overlap": OverlappedMerge over 3 steps of
+    the same shard (fresh table each step, output slots rotating), as bench.py."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    torch.cuda.set_stream(torch.cuda.Stream())
+    import tcbee_amd
+    from tcbee_amd.dist import FlowMerge, OverlappedMerge, shard_range
+    from tracegen import mixed_trace
+
+    tr = mixed_trace(n, seed=404, n_flows=700)
+    lo, hi = shard_range(tr.n, rank, world)
+    sub = tr.slice(lo, hi)
+    m = sub.n
+    arena = torch.zeros(len(sub.arena) + 64, dtype=torch.uint8, device="cuda")
+    arena[:len(sub.arena)] = torch.from_numpy(sub.arena).cuda()
+    off = torch.from_numpy(sub.offset.view(np.int64)).cuda()
+    ln = torch.from_numpy(sub.caplen.view(np.int32)).cuda()
+    ts = torch.from_numpy(sub.ts_ns.view(np.int64)).cuda()
+    nbuf = 2 if mode == "overlap" else 1
+    slots = [{"rec": torch.empty(m * 74 + 64, dtype=torch.uint8, device="cuda"),
+              "hash": torch.empty(m, dtype=torch.int32, device="cuda"),
+              "id": torch.empty(m, dtype=torch.int32, device="cuda"),
+              "n": torch.zeros(1, dtype=torch.int64, device="cuda"),
+              "ctr": torch.zeros(4, dtype=torch.int64, device="cuda")} for _ in range(nbuf)]
+    s = torch.cuda.current_stream().cuda_stream
+    with tcbee_amd.PacketParser(max_frames=max(m, 1), max_flows=cap) as p, \
+            tcbee_amd.PacketParser(max_frames=1024, max_flows=world * cap) as mg:
+        fm = FlowMerge(p, mg, cap, tr.n, nbuf=nbuf)
+        om = OverlappedMerge(fm, nbuf=nbuf) if mode == "overlap" else None
+        steps = 3 if om else 1
+        for i in range(steps):
+            k = i % nbuf
+            b = slots[k]
+            if om:
+                om.acquire(k)
+            b["ctr"].zero_()
+            p.reset_flows(stream=s, sync=False)
+            p.parse_device(arena, len(sub.arena), off, ln, ts, m, b["rec"], m, b["hash"], b["id"],
+                           b["n"], b["ctr"], stream=s)
+            if om:
+                om.submit(k, b["id"], b["n"], m, ctr=b["ctr"])
+            else:
+                fm.step(b["id"], b["n"], m, stream=s)
+                dist.all_reduce(b["ctr"])
+        torch.cuda.synchronize()
+        b = slots[(steps - 1) % nbuf]
+        k = int(b["n"].item())
+        np.savez(os.path.join(result_dir, f"rank{rank}.npz"),
+                 rec=b["rec"][:k * 74].cpu().numpy().reshape(-1, 74),
+                 gids=b["id"][:k].cpu().numpy().view(np.uint32),
+                 ctr=b["ctr"].cpu().numpy(), merged=mg.flows().view(np.uint8))
+    dist.barrier()
+    dist.destroy_process_group()

@@ -1,7 +1,11 @@
 set -u
-mkdir -p gpurun_out/g14
+mkdir -p gpurun_out/g19
 export TMPDIR=/tmp
-W="python tools/k1_sweep.py --frames 100000000 --fpl 2 --workloads imix10k,64B1 --rounds 1 --iters 1 --flows-only"
-timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --output-format csv -d gpurun_out/g14/p1 -o run -- $W > gpurun_out/g14/p1.log 2>&1 || { echo FAIL1; tail -5 gpurun_out/g14/p1.log; exit 1; }
-timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_ACTIVE_INST_VMEM --output-format csv -d gpurun_out/g14/p2 -o run -- $W > gpurun_out/g14/p2.log 2>&1 || { echo FAIL2; tail -5 gpurun_out/g14/p2.log; exit 1; }
-echo ok
+R="python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1"
+timeout -k 10 300 $R --master-port 29541 bench.py --steps 10 --no-cpu --no-extra > gpurun_out/g19/plain.log 2>&1 || { echo FAIL0; tail -20 gpurun_out/g19/plain.log; exit 1; }
+grep '^{' gpurun_out/g19/plain.log | cut -c1-300
+for ov in 0 1; do
+timeout -k 10 300 env TCBEE_BENCH_FORCE_MERGE=1 TCBEE_BENCH_OVERLAP=$ov $R --master-port 2954$ov bench.py --steps 10 --no-cpu --no-extra > gpurun_out/g19/fm_$ov.log 2>&1 || { echo FAIL$ov; tail -20 gpurun_out/g19/fm_$ov.log; exit 1; }
+echo "force-merge overlap=$ov"; grep '^{' gpurun_out/g19/fm_$ov.log | cut -c1-300
+done
+timeout -k 10 300 env TCBEE_BENCH_FORCE_MERGE=1 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/g19/prof -o run -- python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29545 bench.py --steps 5 --no-cpu --no-extra > gpurun_out/g19/prof.log 2>&1 || echo PROF_FAIL

@@ -31,6 +31,7 @@ def main():
     import torch
     import tcbee_amd
     torch.cuda.set_device(0)
+    torch.cuda.set_stream(torch.cuda.Stream())  # non-NULL: NULL means "the ctx's stream"
     stream = torch.cuda.current_stream().cuda_stream
     wl_defs = {"imix10k": ("imix", 1, 10_000), "imix1": ("imix", 0, 1), "64B1": ("64", 0, 1),
                "imix1M": ("imix", 1, 1_000_000), "64B10k": ("64", 1, 10_000)}
