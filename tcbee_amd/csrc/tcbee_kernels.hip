@@ -104,7 +104,23 @@ __device__ __forceinline__ void put_chunk(uint32_t (&w)[24], int c, uint4 v) {
 // arena (the common case) all FPL x 5 loads are issued unconditionally, back to
 // back; otherwise each lane loads only the chunks of [off, off+min(len,54)),
 // bounds-checked. Chunk 5 (IPv6 tail) is loaded later, for IPv6 frames only.
-template <int FPL, bool NOLOAD, bool NT = false>
+// Header-chunk load with an explicit cache policy (A/B of how the L2 fetches a
+// frame's header line; HPOL 0 = the compiler's plain load). Inline asm is not
+// tracked by the compiler's waitcnt insertion: load_windows waits explicitly.
+template <int HPOL>
+__device__ __forceinline__ u32x4 ld_hdr(const u32x4* p) {
+  u32x4 v;
+  if constexpr (HPOL == 1) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  else if constexpr (HPOL == 2) asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+  else if constexpr (HPOL == 3) asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(v) : "v"(p) : "memory");
+  else if constexpr (HPOL == 4) asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1 nt" : "=v"(v) : "v"(p) : "memory");
+  else if constexpr (HPOL == 5) asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+  else if constexpr (HPOL == 6) asm volatile("global_load_dwordx4 %0, %1, off sc0" : "=v"(v) : "v"(p) : "memory");
+  else v = *p;
+  return v;
+}
+
+template <int FPL, bool NOLOAD, bool NT = false, int HPOL = 0>
 __device__ __forceinline__ void load_windows(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                              const uint64_t (&off)[FPL], const uint32_t (&len)[FPL],
                                              uint32_t (&w)[FPL][24]) {
@@ -133,6 +149,7 @@ __device__ __forceinline__ void load_windows(const uint8_t* __restrict__ arena, 
     // all an IPv4 record uses (the MACs and the urgent pointer are never read):
     // 3 or 4 chunks instead of 5, so a window touches one 64-B sector more
     // often. Lanes whose chunk is not needed are masked off the load.
+    u32x4 q[FPL][5];
 #pragma unroll
     for (int f = 0; f < FPL; ++f) {
       const u32x4* src = reinterpret_cast<const u32x4*>(arena + (off[f] & ~15ull));
@@ -141,10 +158,21 @@ __device__ __forceinline__ void load_windows(const uint8_t* __restrict__ arena, 
 #pragma unroll
       for (int c = 0; c < 5; ++c) {
         u32x4 v = {0u, 0u, 0u, 0u};
-        if ((uint32_t)c >= c_lo && (uint32_t)c <= c_hi) v = ld_stream<NT>(src + c);
-        put_chunk(w[f], c, make_uint4(v[0], v[1], v[2], v[3]));
+        if ((uint32_t)c >= c_lo && (uint32_t)c <= c_hi)
+          v = HPOL ? ld_hdr<HPOL>(src + c) : ld_stream<NT>(src + c);
+        q[f][c] = v;
       }
     }
+    if constexpr (HPOL != 0) {
+#pragma unroll
+      for (int f = 0; f < FPL; ++f)
+#pragma unroll
+        for (int c = 0; c < 5; ++c) asm volatile("s_waitcnt vmcnt(0)" : "+v"(q[f][c]) :: "memory");
+    }
+#pragma unroll
+    for (int f = 0; f < FPL; ++f)
+#pragma unroll
+      for (int c = 0; c < 5; ++c) put_chunk(w[f], c, make_uint4(q[f][c][0], q[f][c][1], q[f][c][2], q[f][c][3]));
   } else {
 #pragma unroll
     for (int f = 0; f < FPL; ++f) {
@@ -516,7 +544,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 // look-back; STAGE 1: each wave stages and stores its own 64-record group per
 // round (its records are contiguous in the output), 4.7 KB of LDS per wave.
 // OCC: minimum waves per SIMD requested from the register allocator (0: default)
-template <int FPL, bool FLOWS, int PROBE_AUX, int ABL = 0, int STAGE = 0, bool NT = false, int OCC = 0>
+template <int FPL, bool FLOWS, int PROBE_AUX, int ABL = 0, int STAGE = 0, bool NT = false, int OCC = 0,
+          int HPOL = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, OCC ? 8 : 8)))
 void k_parse(ParseArgs a) {
   constexpr int TILE = kBlock * FPL;
@@ -564,7 +593,7 @@ void k_parse(ParseArgs a) {
   for (int f = 0; f < FPL; ++f) lenc[f] = clamp_caplen(offv[f], clen[f], a.arena_len);
   {
     uint32_t W[FPL][24];
-    load_windows<FPL, (ABL & 4) != 0, NT>(a.arena, a.arena_len, offv, lenc, W);
+    load_windows<FPL, (ABL & 4) != 0, NT, HPOL>(a.arena, a.arena_len, offv, lenc, W);
 #pragma unroll
     for (int f = 0; f < FPL; ++f)
       acc[f] = parse_window<(ABL & 4) != 0>(a.arena, a.arena_len, offv[f], lenc[f], tsv[f],
@@ -1600,6 +1629,11 @@ static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s
       case 1: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 0>), grid, dim3(kBlock), 0, s, a); break;
       case 2: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 5>), grid, dim3(kBlock), 0, s, a); break;
       case 3: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 6>), grid, dim3(kBlock), 0, s, a); break;
+#define TCBEE_HPOL_CASE(P) \
+      case 10 + P: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 0, false, 0, P>), grid, dim3(kBlock), 0, s, a); break;
+      TCBEE_HPOL_CASE(1) TCBEE_HPOL_CASE(2) TCBEE_HPOL_CASE(3) TCBEE_HPOL_CASE(4) TCBEE_HPOL_CASE(5)
+      TCBEE_HPOL_CASE(6)
+#undef TCBEE_HPOL_CASE
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

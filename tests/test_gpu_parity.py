@@ -289,3 +289,35 @@ def test_flow_table_full_reports(gpu):
         res = p.parse(tr)
         assert res.n > 0
         assert p.status() == tcbee_amd._lib.EFLOWFULL
+
+
+def test_batch_over_1M_frames_multibatch(gpu, oracle):
+    """Batches above 1M frames take the 4-kernel rank scan (bounded by the highest
+    first-seen word, bitmap cleared again by K3); three batches, the second one
+    adding flows to a table that already has some."""
+    tr = tcbee_amd.synth_trace(2_600_000, sizes="imix", kind=1, n_flows=6000)
+    cuts = [0, 1_200_000, 2_400_000, 2_600_000]
+    with tcbee_amd.PacketParser(max_frames=1_300_000, max_arena=1 << 30, max_flows=1 << 14) as p:
+        rs = [p.parse(tr.slice(lo, hi)) for lo, hi in zip(cuts, cuts[1:])]
+        rec, fh, fi, ctr, table = oracle.parse(tr)
+        assert np.array_equal(np.concatenate([r.records for r in rs]), rec)
+        assert np.array_equal(np.concatenate([r.flow_id for r in rs]), fi)
+        assert np.array_equal(p.flows(), table)
+
+
+def test_k3_mode_switch_across_batches(gpu, oracle):
+    """A table that grows past K3's LDS bins between batches: batch 1 is counted in
+    mode 0 (<= 12288 flows), batch 2 in mode 1 (bucketed); ids and counts continue."""
+    from tracegen import mixed_trace
+    a = mixed_trace(40_000, seed=31, n_flows=3000)
+    b = mixed_trace(160_000, seed=32, n_flows=40_000)
+    frames = [a.frame(i) for i in range(a.n)] + [b.frame(i) for i in range(b.n)]
+    tr = Trace.from_frames(frames)
+    with tcbee_amd.PacketParser(max_frames=1 << 18, max_arena=1 << 26, max_flows=1 << 17) as p:
+        r1 = p.parse(tr.slice(0, a.n))
+        n1 = p.flow_count()
+        r2 = p.parse(tr.slice(a.n, tr.n))
+        rec, fh, fi, ctr, table = oracle.parse(tr)
+        assert n1 <= 12288 < len(table)
+        assert np.array_equal(np.concatenate([r1.flow_id, r2.flow_id]), fi)
+        assert np.array_equal(p.flows(), table)
