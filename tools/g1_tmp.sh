@@ -1,7 +1,7 @@
 set -u
-mkdir -p gpurun_out/g21
+mkdir -p gpurun_out/g23
 export TMPDIR=/tmp
-timeout -k 10 400 python tools/arena_alloc_ab.py > gpurun_out/g21/ab.log 2>&1 || { echo FAIL1; tail -20 gpurun_out/g21/ab.log; exit 1; }
-tail -4 gpurun_out/g21/ab.log
-timeout -s KILL 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum --output-format csv -d gpurun_out/g21/rd -o run -- python tools/arena_alloc_ab.py --iters 1 > gpurun_out/g21/rd.log 2>&1 || { echo FAIL2; tail -5 gpurun_out/g21/rd.log; exit 1; }
-echo ok
+for r in tmp_old . tmp_old .; do
+timeout -k 10 300 python tools/e2e_ab.py $r >> gpurun_out/g23/e2e.log 2>&1 || { echo FAIL; tail -20 gpurun_out/g23/e2e.log; exit 1; }
+done
+grep Mpkt gpurun_out/g23/e2e.log

@@ -16,7 +16,7 @@ step() {  # name timeout cmd...
 }
 for s in "$@"; do
   case $s in
-    tests)  step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    tests)  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread ;;
     tests-all)  step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 600 python bench.py ;;
