@@ -56,7 +56,7 @@ def build_device_trace(torch, n, sizes, kind, n_flows, seed, first_index, stream
 
 
 def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup, seed,
-               multi=None):
+               multi=None, full_check=False):
     import tcbee_amd
     stream = torch.cuda.current_stream().cuda_stream
     # multi: the N>1 exchange runs (also at N=1 under TCBEE_BENCH_FORCE_MERGE=1, a
@@ -132,7 +132,10 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
              "pkts_total": int(flows["pkts"].sum())}
     if multi:
         check["ingress_global"] = int(last["ctr"][0].item())
-    if rank == 0:
+    if rank == 0 and full_check and not multi:
+        check.update(validate_full(torch, last["rec"], last["hash"], last["id"], n, sizes, kind,
+                                   n_flows, seed, nrec, flows))
+    elif rank == 0:
         check.update(validate_sample(torch, last["rec"], last["hash"], n, sizes, kind, n_flows,
                                      seed, first, nrec))
     p.close()
@@ -141,6 +144,44 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     del d_arena, slots
     torch.cuda.empty_cache()
     return elapsed, k1_ms / max(k1_launches, 1), nrec, check
+
+
+def validate_full(torch, d_rec, d_hash, d_id, n, sizes, kind, n_flows, seed, nrec, gpu_flows,
+                  chunk=2_000_000):
+    """Every record, flow hash and flow id of the timed run vs the oracle streamed over
+    the same trace in chunks (one flow table carried across them), and the whole
+    flow table (untimed; config 3 at N=1)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import tcbee_amd
+    from oracle_py import Oracle
+    orc = Oracle()
+    ft = orc.new_flowtab(1 << 15)
+    t0 = time.perf_counter()
+    ok = nrec == n
+    bad_at = None
+    try:
+        for lo in range(0, n, chunk):
+            hi = min(n, lo + chunk)
+            tr = tcbee_amd.synth_trace(hi - lo, sizes=sizes, kind=kind, n_flows=n_flows,
+                                       seed=seed, first_index=lo)
+            rec, fh, fi, _, _ = orc.parse(tr, ft=ft, record_base=lo)
+            # synthetic frames are all accepted: record index == frame index
+            same = (len(rec) == hi - lo
+                    and np.array_equal(d_rec[lo * 74: hi * 74].cpu().numpy().reshape(-1, 74), rec)
+                    and np.array_equal(d_hash[lo:hi].cpu().numpy().view(np.uint32), fh)
+                    and np.array_equal(d_id[lo:hi].cpu().numpy().view(np.uint32), fi))
+            if not same and bad_at is None:
+                bad_at = lo
+            ok = ok and same
+        table = orc.flows(ft)
+    finally:
+        orc.free_flowtab(ft)
+    table_ok = len(table) == len(gpu_flows) and np.array_equal(table, gpu_flows)
+    out = {"full_bit_exact": bool(ok), "full_records": n, "flow_table_exact": bool(table_ok),
+           "full_check_s": round(time.perf_counter() - t0, 1)}
+    if bad_at is not None:
+        out["first_bad_chunk"] = bad_at
+    return out
 
 
 def validate_sample(torch, d_rec, d_hash, n, sizes, kind, n_flows, seed, first, nrec,
@@ -258,6 +299,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip config-2 and e2e legs")
     ap.add_argument("--e2e-frames", type=int, default=20_000_000)
+    ap.add_argument("--sample-check", action="store_true",
+                    help="N=1: check 2 x 200k records instead of every record + the table")
     args = ap.parse_args()
 
     import torch
@@ -288,7 +331,8 @@ def main():
 
     elapsed, k1_ms, nrec, check = run_device(torch, dist, rank, world, args.frames, args.sizes,
                                              kind, args.flows, args.steps, args.warmup,
-                                             args.seed, multi=world > 1 or force_merge)
+                                             args.seed, multi=world > 1 or force_merge,
+                                             full_check=not args.sample_check)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -323,7 +367,8 @@ def main():
         }
         if not args.no_extra and world == 1:
             e_el, e_k1, e_n, e_chk = run_device(torch, None, 0, 1, 1_000_000, "64", 0, 1,
-                                                max(args.steps, 20), args.warmup, args.seed)
+                                                max(args.steps, 20), args.warmup, args.seed,
+                                                full_check=True)
             out["config2_1M_64B"] = {"mpkts": round(1_000_000 * max(args.steps, 20) / e_el / 1e6, 1),
                                      "ms_per_step": round(e_el / max(args.steps, 20) * 1e3, 4),
                                      "k1_ms": round(e_k1, 4), "check": e_chk}
@@ -331,7 +376,7 @@ def main():
             # appears in every contiguous shard, so each GPU's table holds all 1M
             c4_n, c4_steps = 125_000_000, 5
             c_el, c_k1, c_n, c_chk = run_device(torch, None, 0, 1, c4_n, "imix", 1, 1_000_000,
-                                                c4_steps, 1, args.seed)
+                                                c4_steps, 1, args.seed, full_check=True)
             out["config4_shard_1M_flows"] = {
                 "frames": c4_n, "flows": 1_000_000, "mpkts": round(c4_n * c4_steps / c_el / 1e6, 1),
                 "ms_per_step": round(c_el / c4_steps * 1e3, 4), "k1_ms": round(c_k1, 4),
