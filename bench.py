@@ -55,16 +55,57 @@ def build_device_trace(torch, n, sizes, kind, n_flows, seed, first_index, stream
     return d_arena, alen, d_off, d_len, d_ts
 
 
+def build_shard_trace(torch, n_global, world, rank, sizes, kind, n_flows, seed, stream):
+    """This rank's flow-hash shard of the global synthetic trace [0, n_global) (the
+    NIC-RSS view of config 4), built on the device: global indices + caplens
+    (tcbee_gen_shard_index_device), offsets by a prefix sum, headers by the device
+    generator at each frame's global index."""
+    import tcbee_amd
+    cap = n_global // world + 8 * int(n_global ** 0.5) + (1 << 16)
+    gidx = torch.empty(cap, dtype=torch.int64, device="cuda")
+    clen = torch.empty(cap, dtype=torch.int32, device="cuda")
+    scratch = torch.empty(tcbee_amd.gen_shard_scratch_words(n_global), dtype=torch.int64,
+                          device="cuda")
+    n_out = torch.zeros(1, dtype=torch.int64, device="cuda")
+    tcbee_amd.gen_shard_index_device(n_global, world, rank, kind, n_flows, seed,
+                                     sizes == "imix", gidx, clen, cap, scratch, n_out,
+                                     stream=stream)
+    m = int(n_out.item())
+    if m > cap:
+        raise RuntimeError(f"shard of {m} frames exceeds its buffer ({cap})")
+    gidx, clen = gidx[:m].contiguous(), clen[:m].contiguous()
+    off = torch.zeros(m, dtype=torch.int64, device="cuda")
+    if m > 1:
+        torch.cumsum(clen[:-1].to(torch.int64), 0, out=off[1:])
+    alen = int(off[-1].item() + clen[-1].item()) if m else 0
+    ts = gidx * 1000 + 1_000_000_000  # TS_BASE_NS + TS_STEP_NS * global index
+    arena = torch.zeros(alen + 64, dtype=torch.uint8, device="cuda")
+    tcbee_amd.gen_frames_index_device(arena, off, clen, gidx, m, kind, n_flows, seed,
+                                      stream=stream)
+    torch.cuda.synchronize()
+    del scratch
+    return arena, alen, off, clen, ts, gidx, m
+
+
 def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup, seed,
-               multi=None, full_check=False):
+               multi=None, full_check=False, flowhash=False):
     import tcbee_amd
     stream = torch.cuda.current_stream().cuda_stream
     # multi: the N>1 exchange runs (also at N=1 under TCBEE_BENCH_FORCE_MERGE=1, a
     # one-GPU rehearsal of its cost and of the overlap)
     multi = world > 1 if multi is None else multi
     first = rank * n
-    d_arena, alen, d_off, d_len, d_ts = build_device_trace(torch, n, sizes, kind, n_flows,
-                                                           seed, first, stream)
+    n_global = n * world
+    gidx = None
+    if flowhash:
+        # n frames per GPU on average: rank `rank` parses the frames of ITS flows out of
+        # a global trace of n * world frames (sizes differ by a few hundred)
+        d_arena, alen, d_off, d_len, d_ts, gidx, n = build_shard_trace(
+            torch, n_global, world, rank, sizes, kind, n_flows, seed, stream)
+        first = 0
+    else:
+        d_arena, alen, d_off, d_len, d_ts = build_device_trace(torch, n, sizes, kind, n_flows,
+                                                               seed, first, stream)
     # N>1: two output slots, so that step i's flow-table exchange (side stream) overlaps
     # step i+1's parse (main stream)
     overlap = multi and os.environ.get("TCBEE_BENCH_OVERLAP", "1") != "0"
@@ -74,15 +115,20 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
               "id": torch.empty(n, dtype=torch.int32, device="cuda"),
               "n": torch.zeros(1, dtype=torch.int64, device="cuda"),
               "ctr": torch.zeros(4, dtype=torch.int64, device="cuda")} for _ in range(nbuf)]
-    cap = max(4 * n_flows, 1 << 12)
+    # flow-hash shards hold ~n_flows/world flows each; the exchange carries `xcap`
+    # entries per rank (checked against the real count after the run)
+    flows_here = -(-n_flows // world) if flowhash else n_flows
+    cap = max(4 * flows_here, 1 << 12)
+    xcap = max(int(1.25 * flows_here) + 4096, 1 << 12) if flowhash else cap
     p = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=n, max_arena=0,
                                max_flows=cap)
     merged = om = fm = None
     if multi:
         from tcbee_amd.dist import FlowMerge, OverlappedMerge
         merged = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=1024,
-                                        max_arena=0, max_flows=world * cap)
-        fm = FlowMerge(p, merged, cap, world * n, nbuf=nbuf)
+                                        max_arena=0, max_flows=world * xcap)
+        fm = FlowMerge(p, merged, xcap, n_global if flowhash else world * n, nbuf=nbuf)
+        fm.gidx = gidx
         om = OverlappedMerge(fm, nbuf=nbuf) if overlap else None
     count = [0]
 
@@ -127,12 +173,19 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     # validation (untimed): counts, flow table, and a bit-exact sample vs the oracle
     last = slots[(count[0] - 1) % nbuf]
     nrec = int(last["n"].item())
+    if multi and p.flow_count() > xcap:
+        raise RuntimeError(f"rank {rank}: {p.flow_count()} flows exceed the exchange cap {xcap}")
     flows = (merged if merged is not None else p).flows()
     check = {"records": nrec, "flows": int(len(flows)), "status": status,
              "pkts_total": int(flows["pkts"].sum())}
     if multi:
         check["ingress_global"] = int(last["ctr"][0].item())
-    if rank == 0 and full_check and not multi:
+    if flowhash:
+        check["frames_local"] = n
+        if rank == 0:
+            check.update(validate_shard(torch, last["rec"], last["hash"], last["id"], gidx, n,
+                                        sizes, kind, n_flows, seed, nrec))
+    elif rank == 0 and full_check and not multi:
         check.update(validate_full(torch, last["rec"], last["hash"], last["id"], n, sizes, kind,
                                    n_flows, seed, nrec, flows))
     elif rank == 0:
@@ -143,7 +196,28 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
         merged.close()
     del d_arena, slots
     torch.cuda.empty_cache()
-    return elapsed, k1_ms / max(k1_launches, 1), nrec, check
+    return elapsed, k1_ms / max(k1_launches, 1), nrec, check, n
+
+
+def validate_shard(torch, d_rec, d_hash, d_id, gidx, n, sizes, kind, n_flows, seed, nrec,
+                   sample=200_000):
+    """Flow-hash shard: the first `sample` local records (hash, global flow id) vs the
+    oracle over the global trace prefix that holds them (a flow's global id only
+    depends on the first-seen order up to its own first frame)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import tcbee_amd
+    from oracle_py import Oracle
+    k = min(sample, n)
+    g = gidx[:k].cpu().numpy().astype(np.int64)
+    glob = tcbee_amd.synth_trace(int(g[-1]) + 1, sizes=sizes, kind=kind, n_flows=n_flows,
+                                 seed=seed)
+    rec, fh, fi, _, _ = Oracle().parse(glob)  # every synthetic frame is accepted
+    ok = (nrec == n
+          and np.array_equal(d_rec[:k * 74].cpu().numpy().reshape(-1, 74), rec[g])
+          and np.array_equal(d_hash[:k].cpu().numpy().view(np.uint32), fh[g])
+          and np.array_equal(d_id[:k].cpu().numpy().view(np.uint32), fi[g]))
+    return {"sample_bit_exact": bool(ok), "sample_frames": k,
+            "sample_global_prefix": int(g[-1]) + 1 if k else 0}
 
 
 def validate_full(torch, d_rec, d_hash, d_id, n, sizes, kind, n_flows, seed, nrec, gpu_flows,
@@ -299,9 +373,17 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip config-2 and e2e legs")
     ap.add_argument("--e2e-frames", type=int, default=20_000_000)
+    ap.add_argument("--shard", default="contig", choices=["contig", "flowhash"],
+                    help="N>1 partition: contiguous frame ranges (default) or flow-hash "
+                         "shards of one global trace of frames x N (the NIC-RSS view)")
+    ap.add_argument("--config4", action="store_true",
+                    help="config 4 of BASELINE.json: 125M IMIX frames per GPU, 1M flows, "
+                         "flow-hash shards")
     ap.add_argument("--sample-check", action="store_true",
                     help="N=1: check 2 x 200k records instead of every record + the table")
     args = ap.parse_args()
+    if args.config4:
+        args.frames, args.flows, args.sizes, args.shard = 125_000_000, 1_000_000, "imix", "flowhash"
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -329,10 +411,10 @@ def main():
     torch.cuda.set_stream(torch.cuda.Stream())
     kind = 1 if args.flows > 1 else 0
 
-    elapsed, k1_ms, nrec, check = run_device(torch, dist, rank, world, args.frames, args.sizes,
-                                             kind, args.flows, args.steps, args.warmup,
-                                             args.seed, multi=world > 1 or force_merge,
-                                             full_check=not args.sample_check)
+    elapsed, k1_ms, nrec, check, n_local = run_device(
+        torch, dist, rank, world, args.frames, args.sizes, kind, args.flows, args.steps,
+        args.warmup, args.seed, multi=world > 1 or force_merge,
+        full_check=not args.sample_check, flowhash=args.shard == "flowhash")
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -345,16 +427,18 @@ def main():
     if rank == 0:
         # roofline of the dominant kernel (K1 k_parse), algorithmic bytes per launch
         hdr = V4_HDR_BYTES  # synthetic frames are IPv4/TCP
-        alg_bytes = args.frames * (IDX_BYTES + hdr) + nrec * OUT_BYTES
+        alg_bytes = n_local * (IDX_BYTES + hdr) + nrec * OUT_BYTES
         achieved = alg_bytes / (k1_ms * 1e-3) / 1e9
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mpkt/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": ("config3: IMIX 64/576/1500 7:4:1 IPv4/TCP, "
+            "config": {"workload": (("config4: " if args.config4 else "config3: ")
+                                    + "IMIX 64/576/1500 7:4:1 IPv4/TCP, "
                                     f"{args.flows} flows" if args.sizes == "imix"
                                     else f"64B IPv4/TCP, {args.flows} flow(s)"),
+                       "shard": args.shard,
                        "frames_per_gpu": args.frames, "flows": args.flows,
                        "parallelism": f"shard{world}" + ("+merge" if force_merge and world == 1
                                                          else "")},
@@ -365,8 +449,8 @@ def main():
                          "alg_bytes_per_frame": IDX_BYTES + hdr + OUT_BYTES},
             "check": check,
         }
-        if not args.no_extra and world == 1:
-            e_el, e_k1, e_n, e_chk = run_device(torch, None, 0, 1, 1_000_000, "64", 0, 1,
+        if not args.no_extra and world == 1 and not args.config4:
+            e_el, e_k1, e_n, e_chk, _ = run_device(torch, None, 0, 1, 1_000_000, "64", 0, 1,
                                                 max(args.steps, 20), args.warmup, args.seed,
                                                 full_check=True)
             out["config2_1M_64B"] = {"mpkts": round(1_000_000 * max(args.steps, 20) / e_el / 1e6, 1),
@@ -375,7 +459,7 @@ def main():
             # one GPU's shard of config 4 (1B frames / 8 GPUs, 1M flows): every flow
             # appears in every contiguous shard, so each GPU's table holds all 1M
             c4_n, c4_steps = 125_000_000, 5
-            c_el, c_k1, c_n, c_chk = run_device(torch, None, 0, 1, c4_n, "imix", 1, 1_000_000,
+            c_el, c_k1, c_n, c_chk, _ = run_device(torch, None, 0, 1, c4_n, "imix", 1, 1_000_000,
                                                 c4_steps, 1, args.seed, full_check=True)
             out["config4_shard_1M_flows"] = {
                 "frames": c4_n, "flows": 1_000_000, "mpkts": round(c4_n * c4_steps / c_el / 1e6, 1),

@@ -219,6 +219,22 @@ int tcbee_gen_frames_device(uint8_t* arena_dev, const uint64_t* offset_dev,
 int tcbee_gen_frames_host(uint8_t* arena, const uint64_t* offset,
                           const uint32_t* caplen, uint64_t n, uint64_t first_index,
                           int kind, uint64_t n_flows, uint64_t seed);
+/* As tcbee_gen_frames_device, local frame j being global frame gidx_dev[j]. */
+int tcbee_gen_frames_index_device(uint8_t* arena_dev, const uint64_t* offset_dev,
+                                  const uint32_t* caplen_dev, const uint64_t* gidx_dev,
+                                  uint64_t n, int kind, uint64_t n_flows, uint64_t seed,
+                                  void* stream);
+/* One GPU's flow-hash shard of the global synthetic trace [0, n_global)
+ * (config 4, the NIC-RSS view): the frames whose flow hash satisfies
+ * fold32(flow_hash64(key)) % world == rank, in global order. Writes
+ * out_gidx_dev[k] (global index) and out_caplen_dev[k] (64 B, or IMIX 64/576/1500
+ * when imix != 0, as synth_index) for k < min(count, cap), and *n_out_dev = count.
+ * scratch_dev: tcbee_gen_shard_scratch(n_global) u64 words. Asynchronous. */
+uint64_t tcbee_gen_shard_scratch(uint64_t n_global);
+int tcbee_gen_shard_index_device(uint64_t n_global, int world, int rank, int kind,
+                                 uint64_t n_flows, uint64_t seed, int imix,
+                                 uint64_t* out_gidx_dev, uint32_t* out_caplen_dev, uint64_t cap,
+                                 uint64_t* scratch_dev, uint64_t* n_out_dev, void* stream);
 
 /* ---- ingest pipeline: host frames -> records on the host ----------------
  * (replaces the live ring drain of

@@ -644,6 +644,47 @@ int tcbee_gen_frames_device(uint8_t* arena, const uint64_t* off, const uint32_t*
   return TCBEE_OK;
 }
 
+int tcbee_gen_frames_index_device(uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                                  const uint64_t* gidx, uint64_t n, int kind, uint64_t n_flows,
+                                  uint64_t seed, void* stream) {
+  if ((n && (!arena || !off || !len || !gidx)) || (kind != 0 && kind != 1)) return TCBEE_EINVAL;
+  if (kind == 1 && n_flows == 0) return TCBEE_EINVAL;
+  if (!n) return TCBEE_OK;
+  TRY_HIP(launch_gen(arena, off, len, n, 0, kind, n_flows, seed, (hipStream_t)stream, gidx));
+  return TCBEE_OK;
+}
+
+uint64_t tcbee_gen_shard_scratch(uint64_t n_global) {
+  const uint64_t c = (n_global + kShardChunk - 1) / kShardChunk;
+  return c ? c : 1;
+}
+
+int tcbee_gen_shard_index_device(uint64_t n_global, int world, int rank, int kind,
+                                 uint64_t n_flows, uint64_t seed, int imix, uint64_t* out_gidx,
+                                 uint32_t* out_caplen, uint64_t cap, uint64_t* scratch,
+                                 uint64_t* n_out, void* stream) {
+  if (world < 1 || rank < 0 || rank >= world || (kind != 0 && kind != 1) || !scratch || !n_out ||
+      (cap && (!out_gidx || !out_caplen)))
+    return TCBEE_EINVAL;
+  if (kind == 1 && n_flows == 0) return TCBEE_EINVAL;
+  if ((n_global + kShardChunk - 1) / kShardChunk > 0x7FFFFFFFull) return TCBEE_ECAPACITY;
+  ShardArgs a{};
+  a.n_global = n_global;
+  a.world = (uint32_t)world;
+  a.rank = (uint32_t)rank;
+  a.kind = kind;
+  a.imix = imix;
+  a.n_flows = n_flows;
+  a.seed = seed;
+  a.gidx = out_gidx;
+  a.caplen = out_caplen;
+  a.cap = cap;
+  a.scratch = scratch;
+  a.n_out = n_out;
+  TRY_HIP(launch_shard_index(a, (hipStream_t)stream));
+  return TCBEE_OK;
+}
+
 int tcbee_gen_frames_host(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
                           uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed) {
   if ((n && (!arena || !off || !len)) || (kind != 0 && kind != 1)) return TCBEE_EINVAL;

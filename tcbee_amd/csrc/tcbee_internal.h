@@ -144,9 +144,24 @@ hipError_t launch_finalize(BatchState* b, PersistState* p, uint64_t out_cap,
                            hipStream_t s);
 hipError_t launch_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
                       uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed,
-                      hipStream_t s);
+                      hipStream_t s, const uint64_t* gidx = nullptr);
+struct ShardArgs {
+  uint64_t n_global;
+  uint32_t world, rank;
+  int kind, imix;
+  uint64_t n_flows, seed;
+  uint64_t* gidx;
+  uint32_t* caplen;
+  uint64_t cap;
+  uint64_t* scratch;  // per chunk: count, then exclusive prefix
+  uint64_t* n_out;
+};
+constexpr int kShardPer = 16;  // global indices per thread
+constexpr uint64_t kShardChunk = 256ull * kShardPer;  // one 256-thread block (kBlock)
+hipError_t launch_shard_index(const ShardArgs& a, hipStream_t s);
 
 constexpr int kBlock = 256;
+static_assert(kShardChunk == (uint64_t)kBlock * kShardPer, "shard chunk = one block");
 constexpr int kScanWordsPerBlock = 2048;  // 256 threads x 8 words
 constexpr uint64_t kRankSmallWords = 1024 * 32;  // single-block rank up to 1M frames
 constexpr int kCountBlock = 1024;

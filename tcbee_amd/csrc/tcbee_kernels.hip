@@ -1596,15 +1596,99 @@ __global__ __launch_bounds__(kRemapBlock) void k_remap(uint32_t* ids, uint64_t n
 // synthetic trace headers (payload stays as the caller zeroed it)
 // ---------------------------------------------------------------------------
 __global__ void k_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
-                      uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed) {
+                      uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed,
+                      const uint64_t* gidx) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
     uint8_t h[54];
-    gen_header(h, first_index + i, len[i], kind, n_flows, seed);
+    gen_header(h, gidx ? gidx[i] : first_index + i, len[i], kind, n_flows, seed);
     const uint32_t m = len[i] < 54u ? len[i] : 54u;
     uint8_t* dst = arena + off[i];
     for (uint32_t b = 0; b < m; ++b) dst[b] = h[b];
   }
+}
+
+// ---------------------------------------------------------------------------
+// flow-hash shard of the synthetic trace (config 4: the NIC-RSS view of 8 GPUs)
+// ---------------------------------------------------------------------------
+// caplen of global frame i (== tcbee_amd.trace.synth_index)
+__device__ __forceinline__ uint32_t gen_caplen(uint64_t i, int imix, uint64_t seed) {
+  if (!imix) return 64u;
+  const uint64_t r = splitmix64((seed ^ 0x1A1Eull) + i) % 12u;
+  return r < 7 ? 64u : (r < 11 ? 576u : 1500u);
+}
+// owner GPU of global frame i: its flow hash (the IpTuple K1 builds for this
+// IPv4/TCP frame, xdp.rs:116-127) folded to 32 bits, mod world
+__device__ __forceinline__ uint32_t gen_owner(const ShardArgs& a, uint64_t i) {
+  const GenFields g = gen_fields(i, a.kind, a.n_flows, a.seed);
+  const uint64_t k1 = (uint64_t)bswap32(g.saddr) << 32, k3 = (uint64_t)bswap32(g.daddr) << 32;
+  const uint64_t k4 = (uint64_t)g.sport | ((uint64_t)g.dport << 16) | ((uint64_t)kTcpProtocol << 32);
+  return fold32(flow_hash64(0, k1, 0, k3, k4)) % a.world;
+}
+
+__device__ __forceinline__ uint32_t shard_mine(const ShardArgs& a, uint64_t i0, uint32_t& bits) {
+  bits = 0;
+#pragma unroll 4
+  for (int k = 0; k < kShardPer; ++k) {
+    const uint64_t i = i0 + k;
+    if (i < a.n_global && gen_owner(a, i) == a.rank) bits |= 1u << k;
+  }
+  return (uint32_t)__popc(bits);
+}
+
+__global__ __launch_bounds__(kBlock) void k_shard_count(ShardArgs a) {
+  __shared__ uint32_t s_tmp[4];
+  uint32_t bits;
+  const uint32_t c = shard_mine(a, blockIdx.x * kShardChunk + threadIdx.x * (uint64_t)kShardPer, bits);
+  uint32_t total;
+  (void)block_excl_scan(c, s_tmp, total);
+  if (threadIdx.x == 0) a.scratch[blockIdx.x] = total;
+}
+
+// one block: exclusive prefix over the chunk counts (each thread a contiguous run)
+__global__ __launch_bounds__(kBlock) void k_shard_scan(ShardArgs a, uint64_t nchunks) {
+  __shared__ uint64_t s_sum[kBlock];
+  const uint64_t per = (nchunks + kBlock - 1) / kBlock;
+  const uint64_t lo = threadIdx.x * per, hi = lo + per < nchunks ? lo + per : nchunks;
+  uint64_t sum = 0;
+  for (uint64_t b = lo; b < hi; ++b) sum += a.scratch[b];
+  s_sum[threadIdx.x] = sum;
+  __syncthreads();
+  uint64_t base = 0;
+  for (uint32_t t = 0; t < threadIdx.x; ++t) base += s_sum[t];
+  for (uint64_t b = lo; b < hi; ++b) {
+    const uint64_t c = a.scratch[b];
+    a.scratch[b] = base;
+    base += c;
+  }
+  if (threadIdx.x == kBlock - 1) *a.n_out = base;
+}
+
+__global__ __launch_bounds__(kBlock) void k_shard_write(ShardArgs a) {
+  __shared__ uint32_t s_tmp[4];
+  const uint64_t i0 = blockIdx.x * kShardChunk + threadIdx.x * (uint64_t)kShardPer;
+  uint32_t bits;
+  const uint32_t c = shard_mine(a, i0, bits);
+  uint32_t total;
+  uint64_t pos = a.scratch[blockIdx.x] + block_excl_scan(c, s_tmp, total);
+  while (bits) {
+    const int k = __ffs(bits) - 1;
+    bits &= bits - 1;
+    if (pos < a.cap) {
+      a.gidx[pos] = i0 + k;
+      a.caplen[pos] = gen_caplen(i0 + k, a.imix, a.seed);
+    }
+    ++pos;
+  }
+}
+
+hipError_t launch_shard_index(const ShardArgs& a, hipStream_t s) {
+  const uint64_t nchunks = (a.n_global + kShardChunk - 1) / kShardChunk;
+  if (nchunks == 0) return hipMemsetAsync(a.n_out, 0, sizeof(uint64_t), s);
+  hipLaunchKernelGGL(k_shard_count, dim3((unsigned)nchunks), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL(k_shard_scan, dim3(1), dim3(kBlock), 0, s, a, nchunks);
+  hipLaunchKernelGGL(k_shard_write, dim3((unsigned)nchunks), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -1775,9 +1859,9 @@ hipError_t launch_remap(uint32_t* ids, uint64_t n_max, const uint64_t* n_dev, co
 
 hipError_t launch_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
                       uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed,
-                      hipStream_t s) {
+                      hipStream_t s, const uint64_t* gidx) {
   hipLaunchKernelGGL(k_gen, dim3(grid_for(n, 8192)), dim3(kBlock), 0, s, arena, off, len, n,
-                     first_index, kind, n_flows, seed);
+                     first_index, kind, n_flows, seed, gidx);
   return hipGetLastError();
 }
 

@@ -68,11 +68,25 @@ class FlowMerge:
                     for _ in range(nbuf)]
         self.meta = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(nbuf)]
         self.ids = torch.empty(self.world * cap, dtype=torch.int32, device=dev)
+        # flow-hash shards (set by the caller): global frame index of each local frame
+        self.gidx: torch.Tensor | None = None
 
     def export(self, slot: int = 0, stream: int | None = None) -> None:
         """Snapshot of the local table into export slot `slot` (before the next parse).
-        Pass a non-NULL stream handle: NULL means the context's own stream."""
+        Pass a non-NULL stream handle: NULL means the context's own stream.
+
+        With `gidx` set (flow-hash shards: a rank's frames are a subsequence of the
+        global stream, and its flows are its own), first_seen becomes the global
+        index of the flow's first record and the merge rebases nothing. That needs
+        record k == local frame k, i.e. every frame accepted (true for the synthetic
+        IPv4/TCP traces this mode is built for)."""
         self.local.export_device(self.ent[slot], self.cap, self.meta[slot], stream=stream)
+        if self.gidx is not None:
+            ent, meta = self.ent[slot], self.meta[slot]
+            valid = torch.arange(self.cap, device=ent.device) < meta[0]
+            fs = ent[:, 7].clamp(0, self.gidx.numel() - 1)
+            ent[:, 7] = torch.where(valid, self.gidx[fs], ent[:, 7])
+            meta[1] = 0
 
     def merge(self, slot: int, out_id: torch.Tensor | None, n_dev: torch.Tensor | None,
               n_max: int, stream: int | None = None):

@@ -204,6 +204,29 @@ def gen_frames_device(arena, offset, caplen, n: int, kind: int, n_flows: int, se
         "tcbee_gen_frames_device")
 
 
+def gen_frames_index_device(arena, offset, caplen, gidx, n: int, kind: int, n_flows: int,
+                            seed: int, stream: int | None = None) -> None:
+    """Device generator, local frame j = global frame gidx[j] (a flow-hash shard)."""
+    _lib.check(_lib.lib().tcbee_gen_frames_index_device(
+        _ptr(arena), _ptr(offset), _ptr(caplen), _ptr(gidx), C.c_uint64(n), kind,
+        C.c_uint64(n_flows), C.c_uint64(seed), C.c_void_p(stream or 0)),
+        "tcbee_gen_frames_index_device")
+
+
+def gen_shard_index_device(n_global: int, world: int, rank: int, kind: int, n_flows: int,
+                           seed: int, imix: bool, out_gidx, out_caplen, cap: int, scratch,
+                           n_out, stream: int | None = None) -> None:
+    """Global indices + caplens of rank's flow-hash shard of the synthetic trace."""
+    _lib.check(_lib.lib().tcbee_gen_shard_index_device(
+        C.c_uint64(n_global), world, rank, kind, C.c_uint64(n_flows), C.c_uint64(seed),
+        int(bool(imix)), _ptr(out_gidx), _ptr(out_caplen), C.c_uint64(cap), _ptr(scratch),
+        _ptr(n_out), C.c_void_p(stream or 0)), "tcbee_gen_shard_index_device")
+
+
+def gen_shard_scratch_words(n_global: int) -> int:
+    return int(_lib.lib().tcbee_gen_shard_scratch(C.c_uint64(n_global)))
+
+
 def remap_ids_device(ids, n_max: int, n_dev, id_map, map_len: int,
                      stream: int | None = None) -> None:
     """ids[p] = id_map[ids[p]] for p < min(*n_dev, n_max)."""

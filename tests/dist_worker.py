@@ -43,7 +43,9 @@ def run(rank, world, port, n, cap, result_dir):
 def run_gpu(rank, world, port, n, cap, result_dir, mode):
     """N>1 choreography on the GPU: ranks share device 0 over gloo. mode "step":
     FlowMerge.step on one stream; mode "overlap": OverlappedMerge over 3 steps of
-    the same shard (fresh table each step, output slots rotating), as bench.py."""
+    the same shard (fresh table each step, output slots rotating), as bench.py;
+    mode "flowhash": the rank's flow-hash shard of a synthetic global trace of n
+    frames, built by the device generator, exchanged with global first_seen."""
     import torch
     import torch.distributed as dist
 
@@ -56,15 +58,23 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode):
     from tcbee_amd.dist import FlowMerge, OverlappedMerge, shard_range
     from tracegen import mixed_trace
 
-    tr = mixed_trace(n, seed=404, n_flows=700)
-    lo, hi = shard_range(tr.n, rank, world)
-    sub = tr.slice(lo, hi)
-    m = sub.n
-    arena = torch.zeros(len(sub.arena) + 64, dtype=torch.uint8, device="cuda")
-    arena[:len(sub.arena)] = torch.from_numpy(sub.arena).cuda()
-    off = torch.from_numpy(sub.offset.view(np.int64)).cuda()
-    ln = torch.from_numpy(sub.caplen.view(np.int32)).cuda()
-    ts = torch.from_numpy(sub.ts_ns.view(np.int64)).cuda()
+    gidx = None
+    if mode == "flowhash":
+        import bench
+        s0 = torch.cuda.current_stream().cuda_stream
+        arena, alen, off, ln, ts, gidx, m = bench.build_shard_trace(
+            torch, n, world, rank, "imix", 1, 3000, 0x7CBEE, s0)
+    else:
+        tr = mixed_trace(n, seed=404, n_flows=700)
+        lo, hi = shard_range(tr.n, rank, world)
+        sub = tr.slice(lo, hi)
+        m = sub.n
+        alen = len(sub.arena)
+        arena = torch.zeros(len(sub.arena) + 64, dtype=torch.uint8, device="cuda")
+        arena[:len(sub.arena)] = torch.from_numpy(sub.arena).cuda()
+        off = torch.from_numpy(sub.offset.view(np.int64)).cuda()
+        ln = torch.from_numpy(sub.caplen.view(np.int32)).cuda()
+        ts = torch.from_numpy(sub.ts_ns.view(np.int64)).cuda()
     nbuf = 2 if mode == "overlap" else 1
     slots = [{"rec": torch.empty(m * 74 + 64, dtype=torch.uint8, device="cuda"),
               "hash": torch.empty(m, dtype=torch.int32, device="cuda"),
@@ -74,7 +84,8 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode):
     s = torch.cuda.current_stream().cuda_stream
     with tcbee_amd.PacketParser(max_frames=max(m, 1), max_flows=cap) as p, \
             tcbee_amd.PacketParser(max_frames=1024, max_flows=world * cap) as mg:
-        fm = FlowMerge(p, mg, cap, tr.n, nbuf=nbuf)
+        fm = FlowMerge(p, mg, cap, n, nbuf=nbuf)
+        fm.gidx = gidx
         om = OverlappedMerge(fm, nbuf=nbuf) if mode == "overlap" else None
         steps = 3 if om else 1
         for i in range(steps):
@@ -84,7 +95,7 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode):
                 om.acquire(k)
             b["ctr"].zero_()
             p.reset_flows(stream=s, sync=False)
-            p.parse_device(arena, len(sub.arena), off, ln, ts, m, b["rec"], m, b["hash"], b["id"],
+            p.parse_device(arena, alen, off, ln, ts, m, b["rec"], m, b["hash"], b["id"],
                            b["n"], b["ctr"], stream=s)
             if om:
                 om.submit(k, b["id"], b["n"], m, ctr=b["ctr"])
@@ -95,6 +106,7 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode):
         b = slots[(steps - 1) % nbuf]
         k = int(b["n"].item())
         np.savez(os.path.join(result_dir, f"rank{rank}.npz"),
+                 gidx=(gidx.cpu().numpy() if gidx is not None else np.zeros(0, np.int64)),
                  rec=b["rec"][:k * 74].cpu().numpy().reshape(-1, 74),
                  gids=b["id"][:k].cpu().numpy().view(np.uint32),
                  ctr=b["ctr"].cpu().numpy(), merged=mg.flows().view(np.uint8))
