@@ -88,20 +88,23 @@ def build_shard_trace(torch, n_global, world, rank, sizes, kind, n_flows, seed, 
 
 
 def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup, seed,
-               multi=None, full_check=False, flowhash=False):
+               multi=None, full_check=False, flowhash=False, vworld=0):
     import tcbee_amd
     stream = torch.cuda.current_stream().cuda_stream
     # multi: the N>1 exchange runs (also at N=1 under TCBEE_BENCH_FORCE_MERGE=1, a
     # one-GPU rehearsal of its cost and of the overlap)
     multi = world > 1 if multi is None else multi
     first = rank * n
-    n_global = n * world
+    # vworld (N=1 only): emulate rank 0 of a vworld-GPU flow-hash run (its shard and
+    # its share of the flows), without the exchange
+    sw = vworld if (flowhash and vworld and world == 1) else world
+    n_global = n * sw
     gidx = None
     if flowhash:
         # n frames per GPU on average: rank `rank` parses the frames of ITS flows out of
         # a global trace of n * world frames (sizes differ by a few hundred)
         d_arena, alen, d_off, d_len, d_ts, gidx, n = build_shard_trace(
-            torch, n_global, world, rank, sizes, kind, n_flows, seed, stream)
+            torch, n_global, sw, rank, sizes, kind, n_flows, seed, stream)
         first = 0
     else:
         d_arena, alen, d_off, d_len, d_ts = build_device_trace(torch, n, sizes, kind, n_flows,
@@ -117,7 +120,7 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
               "ctr": torch.zeros(4, dtype=torch.int64, device="cuda")} for _ in range(nbuf)]
     # flow-hash shards hold ~n_flows/world flows each; the exchange carries `xcap`
     # entries per rank (checked against the real count after the run)
-    flows_here = -(-n_flows // world) if flowhash else n_flows
+    flows_here = -(-n_flows // sw) if flowhash else n_flows
     cap = max(4 * flows_here, 1 << 12)
     xcap = max(int(1.25 * flows_here) + 4096, 1 << 12) if flowhash else cap
     p = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=n, max_arena=0,
@@ -184,7 +187,7 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
         check["frames_local"] = n
         if rank == 0:
             check.update(validate_shard(torch, last["rec"], last["hash"], last["id"], gidx, n,
-                                        sizes, kind, n_flows, seed, nrec))
+                                        sizes, kind, n_flows, seed, nrec, global_ids=multi))
     elif rank == 0 and full_check and not multi:
         check.update(validate_full(torch, last["rec"], last["hash"], last["id"], n, sizes, kind,
                                    n_flows, seed, nrec, flows))
@@ -200,10 +203,11 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
 
 
 def validate_shard(torch, d_rec, d_hash, d_id, gidx, n, sizes, kind, n_flows, seed, nrec,
-                   sample=200_000):
-    """Flow-hash shard: the first `sample` local records (hash, global flow id) vs the
+                   sample=200_000, global_ids=True):
+    """Flow-hash shard: the first `sample` local records (hash, flow id) vs the
     oracle over the global trace prefix that holds them (a flow's global id only
-    depends on the first-seen order up to its own first frame)."""
+    depends on the first-seen order up to its own first frame; without the
+    exchange the ids are the shard's own first-seen order)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import tcbee_amd
     from oracle_py import Oracle
@@ -212,10 +216,17 @@ def validate_shard(torch, d_rec, d_hash, d_id, gidx, n, sizes, kind, n_flows, se
     glob = tcbee_amd.synth_trace(int(g[-1]) + 1, sizes=sizes, kind=kind, n_flows=n_flows,
                                  seed=seed)
     rec, fh, fi, _, _ = Oracle().parse(glob)  # every synthetic frame is accepted
+    want = fi[g]
+    if not global_ids and k:
+        # the shard's own dense ids: order of first appearance within the shard
+        u, first = np.unique(want, return_index=True)
+        local = np.empty(len(u), dtype=np.uint32)
+        local[np.argsort(first, kind="stable")] = np.arange(len(u), dtype=np.uint32)
+        want = local[np.searchsorted(u, want)]
     ok = (nrec == n
           and np.array_equal(d_rec[:k * 74].cpu().numpy().reshape(-1, 74), rec[g])
           and np.array_equal(d_hash[:k].cpu().numpy().view(np.uint32), fh[g])
-          and np.array_equal(d_id[:k].cpu().numpy().view(np.uint32), fi[g]))
+          and np.array_equal(d_id[:k].cpu().numpy().view(np.uint32), want))
     return {"sample_bit_exact": bool(ok), "sample_frames": k,
             "sample_global_prefix": int(g[-1]) + 1 if k else 0}
 
@@ -379,6 +390,9 @@ def main():
     ap.add_argument("--config4", action="store_true",
                     help="config 4 of BASELINE.json: 125M IMIX frames per GPU, 1M flows, "
                          "flow-hash shards")
+    ap.add_argument("--virtual-world", type=int, default=0,
+                    help="N=1 with --shard flowhash: run rank 0's shard of a W-GPU job "
+                         "(its frames and flows; no exchange) to measure one GPU's share")
     ap.add_argument("--sample-check", action="store_true",
                     help="N=1: check 2 x 200k records instead of every record + the table")
     args = ap.parse_args()
@@ -414,7 +428,8 @@ def main():
     elapsed, k1_ms, nrec, check, n_local = run_device(
         torch, dist, rank, world, args.frames, args.sizes, kind, args.flows, args.steps,
         args.warmup, args.seed, multi=world > 1 or force_merge,
-        full_check=not args.sample_check, flowhash=args.shard == "flowhash")
+        full_check=not args.sample_check, flowhash=args.shard == "flowhash",
+        vworld=args.virtual_world)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -438,7 +453,8 @@ def main():
                                     + "IMIX 64/576/1500 7:4:1 IPv4/TCP, "
                                     f"{args.flows} flows" if args.sizes == "imix"
                                     else f"64B IPv4/TCP, {args.flows} flow(s)"),
-                       "shard": args.shard,
+                       "shard": args.shard + (f" (rank 0 of {args.virtual_world})"
+                                              if args.virtual_world and world == 1 else ""),
                        "frames_per_gpu": args.frames, "flows": args.flows,
                        "parallelism": f"shard{world}" + ("+merge" if force_merge and world == 1
                                                          else "")},

@@ -263,7 +263,7 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
     c->k3_nb_max = (uint32_t)(nb < kMaxBuckets ? nb : kMaxBuckets);
     c->k3_g2 = c->k3_nb_max > 2u * c->n_cu ? c->k3_nb_max : 2u * c->n_cu;
     if ((e = dalloc(&c->d_k3_region, max_frames)) != hipSuccess) return fail(map_err(e));
-    if ((e = dalloc(&c->d_k3_offs, c->k3_g1max * (c->k3_nb_max + 1))) != hipSuccess)
+    if ((e = dalloc(&c->d_k3_offs, 2ull * c->n_cu * (c->k3_nb_max + 1))) != hipSuccess)
       return fail(map_err(e));
     if ((e = dalloc(&c->d_k3_lpart, 2ull * c->k3_g2 * kBucket)) != hipSuccess)
       return fail(map_err(e));
@@ -416,7 +416,12 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     if (g1 < gmin) g1 = gmin;
     if (g1 == 0) g1 = 1;
     // finalize is folded into k_count's block 0
-    TRY_HIP(launch_count(k, (unsigned)g1, c->d_k3_region ? c->k3_g2 : 0u, s, c->k3_variant));
+    // mode-1 scatter: two 1024-thread workgroups per CU (its offsets rows: 2 n_cu)
+    uint64_t g1s = (in->n + 8191) / 8192;
+    if (g1s > 2ull * c->n_cu) g1s = 2ull * c->n_cu;
+    if (g1s == 0) g1s = 1;
+    TRY_HIP(launch_count(k, (unsigned)g1, (unsigned)g1s, c->d_k3_region ? c->k3_g2 : 0u, s,
+                         c->k3_variant));
   } else {
     TRY_HIP(launch_finalize(c->d_batch, c->d_persist, out_cap, out_n_dev, ctr_dev, cfg->direction, s));
   }

@@ -115,12 +115,14 @@ struct CountArgs {
   uint64_t* part;            // mode 0: [g1][kCountBins] per-block packed bins
   // mode 1 (large tables; region == nullptr disables it)
   uint64_t* region;          // per accepted frame: (claim, caplen), bucket-sorted per block
-  uint32_t* offs;            // [g1][nb_max + 1] bucket offsets inside each block's region
+  uint32_t* offs;            // [g1s][nb_max + 1] bucket offsets inside each block's region
   uint32_t nb_max;           // buckets the context's table can need
   uint64_t* lpart;           // [S][nb * kBucket][2] partial pkts/bytes per claim
 };
-// g1 = k_count blocks; g2 = k_count_bucket blocks (0: mode 1 impossible, not launched)
-hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g2, hipStream_t s, int k3v = 0);
+// g1 = k_count blocks; g1s = k_count_scatter blocks; g2 = k_count_bucket blocks
+// (g2 = 0: mode 1 impossible, neither is launched)
+hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned g2, hipStream_t s,
+                        int k3v = 0);
 
 struct MergeArgs {
   const uint64_t* ent;        // nseg * stride entries, tcbee_flow_entry as u64[8]

@@ -1172,12 +1172,19 @@ __device__ __forceinline__ uint32_t block1024_excl_scan(uint32_t v, uint32_t* s_
 }
 
 // Mode 1, phase 1 (inside k_count): ids out, bucket counts, scan, scatter.
-template <int U, bool PACK>
+// SABL (timing-only ablations, 0 in product launches): 1 no region stores,
+// 2 no second pass, 4 no id gather/stores in the first pass
+template <int U, bool PACK, int SABL = 0>
 __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint64_t nflows,
                               uint32_t* hist, uint32_t* cur, uint32_t* s_w) {
   const uint32_t tid = threadIdx.x;
   const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);
+  // (these ~nb hot LDS counters cost ~0.9 ms per 125M records at 31 buckets —
+  //  4x slower per atomic than K3 mode 0's thousands of bins; replicating each
+  //  counter 8x by lane did not change it: the cost is not same-address
+  //  serialization)
   for (uint32_t b = tid; b < nb; b += kCountBlock) hist[b] = 0;
+  if (tid == 0) hist[kMaxBuckets] = cur[kMaxBuckets] = 0;
   __syncthreads();
   for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
     uint32_t s[U];
@@ -1187,14 +1194,24 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
       s[k] = load_claim<PACK>(c, p < hi ? p : lo);
       if (p >= hi) s[k] = 0xFFFFFFFFu;
     }
-    uint32_t id[U];
+    if (!(SABL & 4)) {
+      uint32_t id[U];
 #pragma unroll
-    for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.cmap[s[k]];
+      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.cmap[s[k]];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
+        if (c.out_id && p < hi && p < c.out_cap) __builtin_nontemporal_store(id[k], &c.out_id[p]);
+      }
+    }
+    // no-flow records bump the spare counter hist[kMaxBuckets]: no branch per record
 #pragma unroll
     for (int k = 0; k < U; ++k) {
-      const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
-      if (c.out_id && p < hi && p < c.out_cap) __builtin_nontemporal_store(id[k], &c.out_id[p]);
-      if (s[k] != 0xFFFFFFFFu) atomicAdd(&hist[s[k] >> kBucketBits], 1u);
+      if (SABL & 8) {
+        asm volatile("" ::"v"(s[k]));
+        continue;
+      }
+      atomicAdd(&hist[s[k] != 0xFFFFFFFFu ? (s[k] >> kBucketBits) : kMaxBuckets], 1u);
     }
   }
   __syncthreads();
@@ -1212,16 +1229,25 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
   }
   if (tid == 0) offs[nb] = total;
   __syncthreads();
+  if (SABL & 2) return;
   for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
-    uint32_t s[U], len[U];
+    uint32_t s[U], len[U], pos[U];
     load_acc<U, PACK>(c, base + tid, lo, hi, s, len);
+    // every cursor bump issued (unconditionally: no-flow records bump the spare
+    // cur[kMaxBuckets]) before the first store, so the LDS round trips overlap
 #pragma unroll
-    for (int k = 0; k < U; ++k) {
-      if (s[k] != 0xFFFFFFFFu) {
-        const uint32_t pos = atomicAdd(&cur[s[k] >> kBucketBits], 1u);
-        c.region[lo + pos] = (uint64_t)s[k] | ((uint64_t)len[k] << 32);
-      }
+    for (int k = 0; k < U; ++k)
+      pos[k] = atomicAdd(&cur[s[k] != 0xFFFFFFFFu ? (s[k] >> kBucketBits) : kMaxBuckets], 1u);
+    if (SABL & 1) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int k = 0; k < U; ++k) x ^= pos[k] ^ len[k];
+      asm volatile("" ::"v"(x));
+      continue;
     }
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      if (s[k] != 0xFFFFFFFFu) c.region[lo + pos[k]] = (uint64_t)s[k] | ((uint64_t)len[k] << 32);
   }
 }
 
@@ -1231,7 +1257,6 @@ template <int U, int ABL3, bool PACK>
 __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   __shared__ uint64_t s_bin[kCountBins];
   __shared__ uint32_t s_map[kCountBins];  // claim index -> dense id
-  __shared__ uint32_t s_w[kCountBlock / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint64_t n_acc = c.batch->n_acc;
   const uint64_t nflows = c.batch->flow_total;
@@ -1259,11 +1284,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   const uint64_t per = count_per(n_acc, gridDim.x);
   const uint64_t lo = (uint64_t)blockIdx.x * per < n_acc ? (uint64_t)blockIdx.x * per : n_acc;
   const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
-  if (mode == 1) {
-    uint32_t* h = reinterpret_cast<uint32_t*>(s_bin);
-    count_scatter<U, PACK>(c, lo, hi, nflows, h, h + kMaxBuckets, s_w);
-    return;
-  }
+  if (mode == 1) return;  // k_count_scatter
   if (mode == 0) {
     for (uint32_t b = tid; b < nflows; b += kCountBlock) {
       s_bin[b] = 0;
@@ -1352,6 +1373,21 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
     uint64_t* part = c.part + (uint64_t)blockIdx.x * kCountBins;
     for (uint32_t b = tid; b < nflows; b += kCountBlock) part[b] = s_bin[b];
   }
+}
+
+// Mode 1, phase 1 as its own launch: 32 KiB of LDS, so two workgroups share a CU
+// (k_count's 144 KiB of bins + map allow one).
+template <int U, bool PACK, int SABL = 0>
+__global__ __launch_bounds__(kCountBlock) void k_count_scatter(CountArgs c) {
+  __shared__ uint32_t s_hist[kMaxBuckets + 1], s_cur[kMaxBuckets + 1];  // + spare counter
+  __shared__ uint32_t s_w[kCountBlock / 64];
+  const uint64_t nflows = c.batch->flow_total;
+  if (count_mode(c, nflows) != 1) return;
+  const uint64_t n_acc = c.batch->n_acc;
+  const uint64_t per = count_per(n_acc, gridDim.x);
+  const uint64_t lo = (uint64_t)blockIdx.x * per < n_acc ? (uint64_t)blockIdx.x * per : n_acc;
+  const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
+  count_scatter<U, PACK, SABL>(c, lo, hi, nflows, s_hist, s_cur, s_w);
 }
 
 // Mode 1, phase 2: workgroup (j, s) histograms bucket j over the segments of K3
@@ -1801,7 +1837,8 @@ hipError_t launch_rank(const RankArgs& r, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g2, hipStream_t s, int k3v) {
+hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned g2, hipStream_t s,
+                        int k3v) {
   const dim3 grid(g1);
   // k3v (TCBEE_K3ABL at context creation): timing-only ablation / tiling A/B
 #define KC(U, A)                                                                     \
@@ -1819,10 +1856,25 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g2, hipStream_
     default: KC(8, 0); break;
   }
 #undef KC
-  if (g2) hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1);
+  if (g2) {
+    const dim3 gs(g1s);
+    switch (k3v) {  // 64 + SABL: timing-only scatter ablations
+      case 65: hipLaunchKernelGGL((k_count_scatter<8, false, 1>), gs, dim3(kCountBlock), 0, s, c); break;
+      case 66: hipLaunchKernelGGL((k_count_scatter<8, false, 2>), gs, dim3(kCountBlock), 0, s, c); break;
+      case 68: hipLaunchKernelGGL((k_count_scatter<8, false, 4>), gs, dim3(kCountBlock), 0, s, c); break;
+      case 70: hipLaunchKernelGGL((k_count_scatter<8, false, 6>), gs, dim3(kCountBlock), 0, s, c); break;
+      case 80: hipLaunchKernelGGL((k_count_scatter<16, false, 0>), gs, dim3(kCountBlock), 0, s, c); break;
+      case 74: hipLaunchKernelGGL((k_count_scatter<8, false, 10>), gs, dim3(kCountBlock), 0, s, c); break;
+      case 78: hipLaunchKernelGGL((k_count_scatter<8, false, 14>), gs, dim3(kCountBlock), 0, s, c); break;
+      default:
+        if (c.pack_bits) hipLaunchKernelGGL((k_count_scatter<8, true>), gs, dim3(kCountBlock), 0, s, c);
+        else hipLaunchKernelGGL((k_count_scatter<8, false>), gs, dim3(kCountBlock), 0, s, c);
+    }
+    hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1s);
+  }
   // mode 0 needs kCountBins threads; mode 1 up to nb_max * kBucket (grid-stride)
   const unsigned gr = g2 ? 1024u : (unsigned)(kCountBins / 256);
-  hipLaunchKernelGGL(k_count_reduce, dim3(gr), dim3(256), 0, s, c, g1, g2);
+  hipLaunchKernelGGL(k_count_reduce, dim3(gr), dim3(256), 0, s, c, g1, g2);  // g1: mode-0 rows
   return hipGetLastError();
 }
 
