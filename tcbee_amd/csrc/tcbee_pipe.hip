@@ -26,6 +26,7 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -152,6 +153,7 @@ struct tcbee_pipe {
   std::vector<Slot> slots;
   Pool* pool = nullptr;
   tcbee_pipe_stats st{};
+  uint64_t prefetch = 32;  // header-window gather: frames ahead (TCBEE_PIPE_PF, 0 = off)
 };
 
 namespace {
@@ -228,10 +230,20 @@ uint64_t chunk_end(const tcbee_pipe* p, const tcbee_frames* in, uint64_t lo) {
 void stage(tcbee_pipe* p, const tcbee_frames* in, Slot& s) {
   const uint64_t lo = s.lo, n = s.hi - s.lo, W = p->cfg.window;
   if (W) {
+    const uint64_t pf = p->prefetch;
     p->pool->run([&](unsigned part, unsigned parts) {
       const uint64_t a = n * part / parts, b = n * (part + 1) / parts;
       for (uint64_t k = a; k < b; ++k) {
         const uint64_t f = lo + k;
+        // the windows are random lines of a multi-GB capture: fetch the lines of the
+        // frame `pf` ahead while this one is copied (host-memory latency bound)
+        if (pf && k + pf < b) {
+          const uint64_t o2 = in->offset[f + pf];
+          if (o2 + W <= in->arena_len) {
+            __builtin_prefetch(in->arena + o2, 0, 0);
+            __builtin_prefetch(in->arena + o2 + W - 1, 0, 0);
+          }
+        }
         const uint32_t len = in->caplen[f];
         const uint64_t o = in->offset[f];
         const uint64_t want = len < W ? len : W;
@@ -339,6 +351,7 @@ int tcbee_pipe_create(tcbee_pipe** out, int device, const tcbee_pipe_cfg* pc,
   if (!p) return TCBEE_ENOMEM;
   p->device = device;
   p->cfg = c;
+  if (const char* e = std::getenv("TCBEE_PIPE_PF")) p->prefetch = std::strtoull(e, nullptr, 10);
   int rc = tcbee_ctx_create(&p->ctx, device, c.chunk_frames, 0, max_flows ? max_flows : 1 << 20);
   if (rc) return free_pipe(p), rc;
   void* cs = nullptr;
