@@ -153,7 +153,7 @@ struct tcbee_pipe {
   std::vector<Slot> slots;
   Pool* pool = nullptr;
   tcbee_pipe_stats st{};
-  uint64_t prefetch = 32;  // header-window gather: frames ahead (TCBEE_PIPE_PF, 0 = off)
+  uint64_t prefetch = 48;  // header-window gather: frames ahead (TCBEE_PIPE_PF, 0 = off)
 };
 
 namespace {
