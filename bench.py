@@ -122,7 +122,9 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     # entries per rank (checked against the real count after the run)
     flows_here = -(-n_flows // sw) if flowhash else n_flows
     cap = max(4 * flows_here, 1 << 12)
-    xcap = max(int(1.25 * flows_here) + 4096, 1 << 12) if flowhash else cap
+    # (a synthetic trace has at most n_flows flows; the exchange is sized to that, not
+    # to the 4x-headroom table)
+    xcap = max(int(1.25 * flows_here) + 4096, 1 << 12)
     p = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=n, max_arena=0,
                                max_flows=cap)
     merged = om = fm = None
