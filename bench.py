@@ -474,6 +474,13 @@ def main():
             out["config2_1M_64B"] = {"mpkts": round(1_000_000 * max(args.steps, 20) / e_el / 1e6, 1),
                                      "ms_per_step": round(e_el / max(args.steps, 20) * 1e3, 4),
                                      "k1_ms": round(e_k1, 4), "check": e_chk}
+            # config 3's second run: same frames, flows drawn Zipf(1.1)
+            z_el, z_k1, z_n, z_chk, _ = run_device(torch, None, 0, 1, args.frames, args.sizes, 2,
+                                                args.flows, args.steps, args.warmup, args.seed,
+                                                full_check=not args.sample_check)
+            out["config3_zipf"] = {"mpkts": round(args.frames * args.steps / z_el / 1e6, 1),
+                                   "ms_per_step": round(z_el / args.steps * 1e3, 4),
+                                   "k1_ms": round(z_k1, 4), "zipf_s": 1.1, "check": z_chk}
             # one GPU's shard of config 4 (1B frames / 8 GPUs, 1M flows): every flow
             # appears in every contiguous shard, so each GPU's table holds all 1M
             c4_n, c4_steps = 125_000_000, 5

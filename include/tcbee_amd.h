@@ -219,6 +219,18 @@ int tcbee_gen_frames_device(uint8_t* arena_dev, const uint64_t* offset_dev,
 int tcbee_gen_frames_host(uint8_t* arena, const uint64_t* offset,
                           const uint32_t* caplen, uint64_t n, uint64_t first_index,
                           int kind, uint64_t n_flows, uint64_t seed);
+/* Zipf flow mix (config 3, second run): as kind 1, but frame i's flow is the
+ * first k with zcdf[k] > splitmix64(seed + 0x1000 + i), zcdf = n_flows u64
+ * CDF words (non-decreasing, last = 2^64-1; tcbee_amd.trace.zipf_cdf builds the
+ * s = 1.1 table). zcdf_dev is a device pointer for _device, a host one for _host;
+ * both generators produce identical bytes from identical tables. */
+int tcbee_gen_frames_zipf_device(uint8_t* arena_dev, const uint64_t* offset_dev,
+                                 const uint32_t* caplen_dev, uint64_t n, uint64_t first_index,
+                                 uint64_t n_flows, uint64_t seed, const uint64_t* zcdf_dev,
+                                 void* stream);
+int tcbee_gen_frames_zipf_host(uint8_t* arena, const uint64_t* offset, const uint32_t* caplen,
+                               uint64_t n, uint64_t first_index, uint64_t n_flows,
+                               uint64_t seed, const uint64_t* zcdf);
 /* As tcbee_gen_frames_device, local frame j being global frame gidx_dev[j]. */
 int tcbee_gen_frames_index_device(uint8_t* arena_dev, const uint64_t* offset_dev,
                                   const uint32_t* caplen_dev, const uint64_t* gidx_dev,

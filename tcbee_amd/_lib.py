@@ -119,6 +119,11 @@ _SIGS = {
     "tcbee_gen_frames_index_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                                 C.c_uint64, C.c_int, C.c_uint64, C.c_uint64,
                                                 C.c_void_p]),
+    "tcbee_gen_frames_zipf_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                               C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p,
+                                               C.c_void_p]),
+    "tcbee_gen_frames_zipf_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                             C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p]),
     "tcbee_gen_shard_scratch": (C.c_uint64, [C.c_uint64]),
     "tcbee_gen_shard_index_device": (C.c_int, [C.c_uint64, C.c_int, C.c_int, C.c_int,
                                                C.c_uint64, C.c_uint64, C.c_int, C.c_void_p,

@@ -659,6 +659,28 @@ int tcbee_gen_frames_index_device(uint8_t* arena, const uint64_t* off, const uin
   return TCBEE_OK;
 }
 
+int tcbee_gen_frames_zipf_device(uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                                 uint64_t n, uint64_t first_index, uint64_t n_flows,
+                                 uint64_t seed, const uint64_t* zcdf, void* stream) {
+  if ((n && (!arena || !off || !len)) || n_flows == 0 || !zcdf) return TCBEE_EINVAL;
+  if (!n) return TCBEE_OK;
+  TRY_HIP(launch_gen(arena, off, len, n, first_index, kGenZipf, n_flows, seed,
+                     (hipStream_t)stream, nullptr, zcdf));
+  return TCBEE_OK;
+}
+
+int tcbee_gen_frames_zipf_host(uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                               uint64_t n, uint64_t first_index, uint64_t n_flows, uint64_t seed,
+                               const uint64_t* zcdf) {
+  if ((n && (!arena || !off || !len)) || n_flows == 0 || !zcdf) return TCBEE_EINVAL;
+  for (uint64_t i = 0; i < n; ++i) {
+    uint8_t h[54];
+    gen_header(h, first_index + i, len[i], kGenZipf, n_flows, seed, zcdf);
+    std::memcpy(arena + off[i], h, len[i] < 54u ? len[i] : 54u);
+  }
+  return TCBEE_OK;
+}
+
 uint64_t tcbee_gen_shard_scratch(uint64_t n_global) {
   const uint64_t c = (n_global + kShardChunk - 1) / kShardChunk;
   return c ? c : 1;

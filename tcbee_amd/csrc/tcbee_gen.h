@@ -7,7 +7,11 @@
 
 namespace tcbee {
 
-enum GenKind : int { kGenSingleFlow = 0, kGenMultiFlow = 1 };
+// kGenZipf: flow f drawn with P(f) ∝ 1/(f+1)^s through a caller-supplied CDF
+// table (SURVEY.md §8(d) config 3 "second run", s = 1.1): zcdf[k] ≈
+// 2^64 · Σ_{j≤k} p_j, non-decreasing, zcdf[n_flows-1] = 2^64-1, built on the
+// host (tcbee_amd/trace.py zipf_cdf) and read identically by host and device.
+enum GenKind : int { kGenSingleFlow = 0, kGenMultiFlow = 1, kGenZipf = 2 };
 
 struct GenFields {
   uint32_t saddr, daddr;  // numeric (a.b.c.d = a<<24 ...)
@@ -16,7 +20,18 @@ struct GenFields {
   uint8_t flags;
 };
 
-TCBEE_HD GenFields gen_fields(uint64_t i, int kind, uint64_t n_flows, uint64_t seed) {
+// First k with zcdf[k] > r (n ≥ 1; r = 2^64-1 maps to the last flow).
+TCBEE_HD uint64_t zipf_pick(uint64_t r, const uint64_t* zcdf, uint64_t n) {
+  uint64_t lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (zcdf[mid] > r) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
+TCBEE_HD GenFields gen_fields(uint64_t i, int kind, uint64_t n_flows, uint64_t seed,
+                              const uint64_t* zcdf = nullptr) {
   GenFields g;
   if (kind == kGenSingleFlow) {
     // config 2 of BASELINE.json / SURVEY.md §8(d)
@@ -31,7 +46,8 @@ TCBEE_HD GenFields gen_fields(uint64_t i, int kind, uint64_t n_flows, uint64_t s
     g.check = (uint16_t)(((uint32_t)i * 2654435761u) >> 16);
   } else {
     const uint64_t r = splitmix64(seed + 0x1000ULL + i);
-    const uint64_t f = n_flows ? r % n_flows : 0;
+    const uint64_t f = (kind == kGenZipf && zcdf && n_flows) ? zipf_pick(r, zcdf, n_flows)
+                       : (n_flows ? r % n_flows : 0);
     const uint64_t fh = splitmix64((seed << 1) ^ (0xF10F10000000ULL + f));
     g.saddr = 0x0A000000u | (uint32_t)(fh & 0xFFFFFFu);
     g.daddr = 0xAC100000u | (uint32_t)((fh >> 24) & 0xFFFFFu);
@@ -51,8 +67,8 @@ TCBEE_HD GenFields gen_fields(uint64_t i, int kind, uint64_t n_flows, uint64_t s
 // Writes the 54 header bytes (eth + IPv4 + TCP, IHL 5, doff 5) of a frame of
 // `caplen` bytes.
 TCBEE_HD void gen_header(uint8_t* h, uint64_t i, uint32_t caplen, int kind, uint64_t n_flows,
-                         uint64_t seed) {
-  const GenFields g = gen_fields(i, kind, n_flows, seed);
+                         uint64_t seed, const uint64_t* zcdf = nullptr) {
+  const GenFields g = gen_fields(i, kind, n_flows, seed, zcdf);
   // ethernet: dst 02:00:00:00:00:02, src 02:00:00:00:00:01, type IPv4
   h[0] = 0x02; h[1] = 0; h[2] = 0; h[3] = 0; h[4] = 0; h[5] = 0x02;
   h[6] = 0x02; h[7] = 0; h[8] = 0; h[9] = 0; h[10] = 0; h[11] = 0x01;

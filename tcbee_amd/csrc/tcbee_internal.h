@@ -146,7 +146,8 @@ hipError_t launch_finalize(BatchState* b, PersistState* p, uint64_t out_cap,
                            hipStream_t s);
 hipError_t launch_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
                       uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed,
-                      hipStream_t s, const uint64_t* gidx = nullptr);
+                      hipStream_t s, const uint64_t* gidx = nullptr,
+                      const uint64_t* zcdf = nullptr);
 struct ShardArgs {
   uint64_t n_global;
   uint32_t world, rank;

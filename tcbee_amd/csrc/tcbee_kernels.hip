@@ -1633,11 +1633,11 @@ __global__ __launch_bounds__(kRemapBlock) void k_remap(uint32_t* ids, uint64_t n
 // ---------------------------------------------------------------------------
 __global__ void k_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
                       uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed,
-                      const uint64_t* gidx) {
+                      const uint64_t* gidx, const uint64_t* zcdf) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
     uint8_t h[54];
-    gen_header(h, gidx ? gidx[i] : first_index + i, len[i], kind, n_flows, seed);
+    gen_header(h, gidx ? gidx[i] : first_index + i, len[i], kind, n_flows, seed, zcdf);
     const uint32_t m = len[i] < 54u ? len[i] : 54u;
     uint8_t* dst = arena + off[i];
     for (uint32_t b = 0; b < m; ++b) dst[b] = h[b];
@@ -1911,9 +1911,9 @@ hipError_t launch_remap(uint32_t* ids, uint64_t n_max, const uint64_t* n_dev, co
 
 hipError_t launch_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
                       uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed,
-                      hipStream_t s, const uint64_t* gidx) {
+                      hipStream_t s, const uint64_t* gidx, const uint64_t* zcdf) {
   hipLaunchKernelGGL(k_gen, dim3(grid_for(n, 8192)), dim3(kBlock), 0, s, arena, off, len, n,
-                     first_index, kind, n_flows, seed, gidx);
+                     first_index, kind, n_flows, seed, gidx, zcdf);
   return hipGetLastError();
 }
 

@@ -197,7 +197,21 @@ class PacketParser:
 
 def gen_frames_device(arena, offset, caplen, n: int, kind: int, n_flows: int, seed: int,
                       stream: int | None = None, first_index: int = 0) -> None:
-    """Device generator: header bytes of frames whose index is already in HBM."""
+    """Device generator: header bytes of frames whose index is already in HBM.
+    kind 2 (Zipf) ships the CDF table (trace.zipf_cdf) to the device first."""
+    if kind == 2:
+        import torch
+        from .trace import zipf_cdf
+        z = torch.from_numpy(zipf_cdf(n_flows).view(np.int64).copy()).to(arena.device)
+        # the table copy (torch's stream) lands before the kernel (`stream`), and z
+        # stays alive until the kernel is done: synchronous on both sides
+        torch.cuda.synchronize(arena.device)
+        _lib.check(_lib.lib().tcbee_gen_frames_zipf_device(
+            _ptr(arena), _ptr(offset), _ptr(caplen), C.c_uint64(n), C.c_uint64(first_index),
+            C.c_uint64(n_flows), C.c_uint64(seed), _ptr(z), C.c_void_p(stream or 0)),
+            "tcbee_gen_frames_zipf_device")
+        torch.cuda.synchronize(arena.device)
+        return
     _lib.check(_lib.lib().tcbee_gen_frames_device(
         _ptr(arena), _ptr(offset), _ptr(caplen), C.c_uint64(n), C.c_uint64(first_index), kind,
         C.c_uint64(n_flows), C.c_uint64(seed), C.c_void_p(stream or 0)),

@@ -25,6 +25,8 @@ DEFAULT_SEED = 0x7CBEE
 
 GEN_SINGLE = 0
 GEN_MULTI = 1
+GEN_ZIPF = 2     # config 3 "second run": flows drawn Zipf(ZIPF_S)
+ZIPF_S = 1.1
 
 
 @dataclass
@@ -108,9 +110,41 @@ def synth_index(n: int, sizes: str = "64", seed: int = DEFAULT_SEED, first_index
     return offset, caplen, ts, arena_len
 
 
+_ZIPF_CACHE: dict = {}
+
+
+def zipf_cdf(n_flows: int, s: float = ZIPF_S) -> np.ndarray:
+    """CDF table of the Zipf flow mix (tcbee_gen.h kGenZipf): u64 word k ≈
+    2^64 · P(flow ≤ k) with P(flow = k) ∝ (k + 1)^-s, non-decreasing, last word
+    2^64 - 1. Frame i takes the first flow whose word exceeds its 64-bit draw."""
+    key = (int(n_flows), float(s))
+    z = _ZIPF_CACHE.get(key)
+    if z is None:
+        if n_flows < 1:
+            raise ValueError("n_flows must be >= 1")
+        p = np.arange(1, n_flows + 1, dtype=np.float64) ** -float(s)
+        c = np.cumsum(p)
+        c /= c[-1]
+        # 2^64 - 4096: the largest float64 below 2^64 (the cast of 2^64 is undefined)
+        z = np.minimum(c * 2.0 ** 64, 2.0 ** 64 - 4096.0).astype(np.uint64)
+        z[-1] = np.uint64(0xFFFFFFFFFFFFFFFF)
+        z.setflags(write=False)
+        _ZIPF_CACHE[key] = z
+    return z
+
+
 def gen_frames_host(arena: np.ndarray, offset: np.ndarray, caplen: np.ndarray,
                     kind: int, n_flows: int, seed: int, first_index: int = 0) -> None:
     """Writes the header bytes of every frame into ``arena`` (payload untouched)."""
+    if kind == GEN_ZIPF:
+        z = zipf_cdf(n_flows)
+        rc = _lib.lib().tcbee_gen_frames_zipf_host(
+            arena.ctypes.data_as(C.c_void_p), offset.ctypes.data_as(C.c_void_p),
+            caplen.ctypes.data_as(C.c_void_p), C.c_uint64(len(offset)),
+            C.c_uint64(first_index), C.c_uint64(n_flows), C.c_uint64(seed),
+            z.ctypes.data_as(C.c_void_p))
+        _lib.check(rc, "tcbee_gen_frames_zipf_host")
+        return
     rc = _lib.lib().tcbee_gen_frames_host(
         arena.ctypes.data_as(C.c_void_p), offset.ctypes.data_as(C.c_void_p),
         caplen.ctypes.data_as(C.c_void_p), C.c_uint64(len(offset)), C.c_uint64(first_index),
