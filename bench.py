@@ -308,6 +308,23 @@ def cpu_baseline(sizes, kind, n_flows, seed, seconds, threads, sample_n=2_000_00
             if el >= seconds / (2 if t == 1 and threads > 1 else 1):
                 break
         out[t] = (done / el / 1e6, done, el)
+    # CPU-1-file: one thread through the drain task's buffered file
+    # path (orc_baseline_file), xdp.tcp on tmpfs; the file is removed between reps
+    import shutil
+    import tempfile
+    d = tempfile.mkdtemp(prefix="tcbee_cpu_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    try:
+        path = os.path.join(d, "xdp.tcp")
+        done, el = 0, 0.0
+        while el < seconds / 4:
+            t0 = time.perf_counter()
+            orc.baseline_file(tr, path)
+            el += time.perf_counter() - t0
+            done += tr.n
+            os.unlink(path)
+        out["file"] = (done / el / 1e6, done, el)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
     return out, tr.n
 
 
@@ -350,6 +367,57 @@ def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=5, threads=16):
             r = p.parse(sub)
         el = (time.perf_counter() - t0) / 3
     out["parse_batch"] = {"mpkts": round(m / el / 1e6, 1), "frames": m}
+    return out
+
+
+def config5_replay(seed, n=1_000_000, n_flows=4, threads=16):
+    """Config 5 of BASELINE.json: a trace file replayed end to end — classic pcap
+    (tmpfs) -> tcbee_pipe (H2D, K1-K3, D2H) -> xdp.tcp -> the tcbee-process stage
+    into SQLite (records pre-grouped by the GPU's flow ids) -> metrics.json. Each
+    leg is run twice and the second (warm: library loads, device context) timed;
+    it includes pipeline setup (pinned staging) and file creation, as a replay
+    does. Checked: the .tcp bytes equal the oracle's records, the database holds
+    n_flows flows."""
+    import shutil
+    import sqlite3
+    import tempfile
+
+    import tcbee_amd
+    from tcbee_amd import host
+    from tcbee_amd.pipeline import replay_pcap
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_py import Oracle
+    tr = tcbee_amd.synth_trace(n, sizes="64", kind=1 if n_flows > 1 else 0, n_flows=n_flows,
+                               seed=seed)
+    d = tempfile.mkdtemp(prefix="tcbee_c5_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    out = {"frames": n, "flows": n_flows, "frame_bytes": 64, "threads": threads}
+    try:
+        pcap = os.path.join(d, "trace.pcap")
+        host.write_pcap(pcap, tr)
+        for name, with_db in (("pcap_to_tcp", False), ("pcap_to_sqlite", True)):
+            for rep in range(2):
+                prefix = os.path.join(d, f"{name}{rep}_")
+                db = prefix + "tcbee.sqlite" if with_db else None
+                t0 = time.perf_counter()
+                r = replay_pcap(pcap, prefix, db_path=db, threads=threads)
+                el = time.perf_counter() - t0
+            out[name] = {"mpkts": round(n / el / 1e6, 3), "s": round(el, 3),
+                         "records": r["records"]}
+            if with_db:
+                out[name]["sink"] = r.get("sink")
+                con = sqlite3.connect(db)
+                try:
+                    out[name]["db_flows"] = int(con.execute("select count(*) from flows")
+                                                .fetchone()[0])
+                finally:
+                    con.close()
+        rec = Oracle().parse(tr)[0]
+        tcp = np.fromfile(os.path.join(d, "pcap_to_tcp1_xdp.tcp"), dtype=np.uint8)
+        out["check"] = {"tcp_bytes_exact": bool(tcp.size == rec.size
+                                                and np.array_equal(tcp, rec.reshape(-1))),
+                        "db_flows_ok": out["pcap_to_sqlite"].get("db_flows") == n_flows}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
     return out
 
 
@@ -492,6 +560,7 @@ def main():
                 "check": c_chk}
             out["e2e_host"] = host_e2e(args.sizes, kind, args.flows, args.seed,
                                        n=args.e2e_frames)
+            out["config5_replay"] = config5_replay(args.seed)
         if not args.no_cpu and world == 1:
             threads = min(16, os.cpu_count() or 1)
             res, sample_n = cpu_baseline(args.sizes, kind, args.flows, args.seed,
@@ -502,7 +571,10 @@ def main():
                 "sample": (f"{sample_n} frames of the same workload, repeated {done // sample_n}x "
                            f"({el:.1f}s); oracle/tcbee_oracle.c orc_baseline_run = xdp_hook + "
                            "per-thread FLOWS(100) + bincode serialize"),
-                "single_thread": round(res[1][0], 2)}
+                "single_thread": round(res[1][0], 2),
+                "single_thread_file": round(res["file"][0], 2),
+                "file_sample": "1 thread, records appended to tmpfs xdp.tcp through a 720000-B "
+                               "buffer (handlers/mod.rs:70-139)"}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

@@ -9,9 +9,12 @@
  */
 #include "tcbee_oracle.h"
 
+#include <errno.h>
+#include <fcntl.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 /* config.rs:22-33 */
 enum {
@@ -537,4 +540,64 @@ uint64_t orc_baseline_run(const uint8_t* arena, const uint64_t* offset, const ui
     uint64_t total = 0;
     for (int t = 0; t < threads; ++t) total += jobs[t].written;
     return total;
+}
+
+/* CPU-1-file baseline: one thread, xdp_hook + FLOWS(100) as above,
+ * and the drain task's file path: the file opened create|append|O_NONBLOCK
+ * (handlers/mod.rs:70-76), a BufWriter of size_of::<tcp_packet_trace>() x
+ * WRITER_BUFFER_SIZE = 72 x 10000 B (mod.rs:86-89, config.rs:5), and per record
+ * two writes into it — the 70-B bincode body, then FF FF FF FF (mod.rs:126-139)
+ * — a write(2) of the buffer whenever the next piece does not fit, and a final
+ * flush. Returns records written, or ~0 on an I/O error. */
+static int base_put(int fd, uint8_t* buf, size_t* len, size_t cap, const uint8_t* p, size_t k) {
+    if (*len + k > cap) {
+        size_t off = 0;
+        while (off < *len) {
+            const ssize_t w = write(fd, buf + off, *len - off);
+            if (w < 0) {
+                if (errno == EAGAIN || errno == EINTR) continue;
+                return -1;
+            }
+            off += (size_t)w;
+        }
+        *len = 0;
+    }
+    if (k) memcpy(buf + *len, p, k);
+    *len += k;
+    return 0;
+}
+
+uint64_t orc_baseline_file(const uint8_t* arena, const uint64_t* offset, const uint32_t* caplen,
+                           const uint64_t* ts, uint64_t n, uint16_t filter_port,
+                           const char* path) {
+    enum { kCap = 72 * 10000 };
+    const int fd = open(path, O_CREAT | O_WRONLY | O_APPEND | O_NONBLOCK, 0644);
+    if (fd < 0) return ~0ull;
+    uint8_t* buf = (uint8_t*)malloc(kCap);
+    if (!buf) {
+        close(fd);
+        return ~0ull;
+    }
+    uint8_t keys[MAX_FLOWS][40];
+    uint64_t nkeys = 0, w = 0;
+    size_t len = 0;
+    int err = 0;
+    for (uint64_t i = 0; i < n && !err; ++i) {
+        orc_trace t;
+        orc_iptuple k;
+        if (!orc_xdp_hook(arena + offset[i], caplen[i], ts[i], filter_port, &t, &k)) continue;
+        uint8_t key[40];
+        orc_key40(&k, key);
+        int seen = 0;
+        for (uint64_t q = 0; q < nkeys && !seen; ++q) seen = !memcmp(keys[q], key, 40);
+        if (!seen && nkeys < MAX_FLOWS) memcpy(keys[nkeys++], key, 40);
+        uint8_t rec[74];
+        orc_serialize(&t, rec);  /* body [0,70) + marker [70,74) */
+        err = base_put(fd, buf, &len, kCap, rec, 70) || base_put(fd, buf, &len, kCap, rec + 70, 4);
+        w++;
+    }
+    if (!err) err = base_put(fd, buf, &len, 0, NULL, 0);  /* cap 0: flush what is left */
+    free(buf);
+    close(fd);
+    return err ? ~0ull : w;
 }

@@ -121,6 +121,11 @@ uint64_t orc_parse_batch(const uint8_t* arena, const uint64_t* offset,
 uint64_t orc_baseline_run(const uint8_t* arena, const uint64_t* offset,
                           const uint32_t* caplen, const uint64_t* ts, uint64_t n,
                           uint16_t filter_port, int threads, uint8_t* out_rec);
+/* CPU-1-file: one thread, records appended to `path` through the drain task's
+ * 720 000-B buffered writer. Records written, ~0 on I/O error. */
+uint64_t orc_baseline_file(const uint8_t* arena, const uint64_t* offset,
+                           const uint32_t* caplen, const uint64_t* ts, uint64_t n,
+                           uint16_t filter_port, const char* path);
 
 /* Reference FLOWS semantics: the first `max` (100, config.rs:19) distinct
  * IpTuples in arrival order. Writes 40-B keys, returns count. */

@@ -79,6 +79,8 @@ class Oracle:
         L.orc_parse_batch.restype = u64
         L.orc_baseline_run.argtypes = [vp, vp, vp, vp, u64, C.c_uint16, C.c_int, vp]
         L.orc_baseline_run.restype = u64
+        L.orc_baseline_file.argtypes = [vp, vp, vp, vp, u64, C.c_uint16, C.c_char_p]
+        L.orc_baseline_file.restype = u64
         L.orc_ref_flows.argtypes = [vp, vp, vp, u64, C.c_uint16, C.c_int, u64, vp]
         L.orc_ref_flows.restype = u64
         self.L = L
@@ -164,6 +166,16 @@ class Oracle:
         if own:
             self.free_flowtab(ft)
         return rec[:k], fh[:k], fi[:k], ctr.as_dict(), table
+
+    def baseline_file(self, trace, path: str, filter_port: int = 0) -> int:
+        """CPU-1-file: one thread, records appended to `path` (drain-task buffering)."""
+        import os
+        k = self.L.orc_baseline_file(trace.arena.ctypes.data, trace.offset.ctypes.data,
+                                     trace.caplen.ctypes.data, trace.ts_ns.ctypes.data,
+                                     trace.n, filter_port, os.fsencode(path))
+        if k == 0xFFFFFFFFFFFFFFFF:
+            raise OSError(f"orc_baseline_file: I/O error on {path}")
+        return int(k)
 
     def baseline(self, trace, threads: int = 1, filter_port: int = 0):
         out = np.empty((max(trace.n, 1), 74), dtype=np.uint8)

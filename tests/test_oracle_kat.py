@@ -114,3 +114,17 @@ def test_baseline_matches_batch_records(oracle):
     rec = oracle.parse(tr)[0]
     assert oracle.baseline(tr, threads=1) == len(rec)
     assert oracle.baseline(tr, threads=4) == len(rec)
+
+
+def test_baseline_file_writes_the_records(oracle, tmp_path):
+    """CPU-1-file: the drain-task file path appends exactly the batch records,
+    across many 720 000-B buffer flushes, and appends again on a second run."""
+    from tracegen import mixed_trace
+    tr = mixed_trace(30_000, seed=6)
+    rec = oracle.parse(tr)[0]
+    path = str(tmp_path / "xdp.tcp")
+    assert oracle.baseline_file(tr, path) == len(rec)
+    got = np.fromfile(path, dtype=np.uint8)
+    assert np.array_equal(got, rec.reshape(-1))
+    assert oracle.baseline_file(tr.slice(0, 10), path) == len(oracle.parse(tr.slice(0, 10))[0])
+    assert np.fromfile(path, dtype=np.uint8).size > got.size
