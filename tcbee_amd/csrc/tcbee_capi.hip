@@ -22,10 +22,10 @@ struct tcbee_ctx {
   bool reset_pending = false;   // tcbee_flow_reset_device: applied by the next launch
   uint32_t withhold_every = 0;  // TCBEE_TEST_WITHHOLD (look-back recount test hook)
   int k3_no_bucket = 0;         // TCBEE_TEST_K3_NOBUCKET=1: large tables use K3 mode 2 (test hook)
-  int k3_variant = 0;
+  int k3_variant = 0;           // TCBEE_K3ABL: timing-only K3 ablations / tilings (A/B)
   int k1_variant = 0;           // TCBEE_K1V: K1 staging/occupancy A/B variants
   uint32_t plain_walk = kPlainWalk;  // TCBEE_WALK: K1 plain probe walk length (A/B)
-  uint32_t pack_bits = 0;            // K1->K3 scratch packing (0: two words per record)           // TCBEE_K3ABL: timing-only K3 ablations / tilings (A/B)
+  uint32_t pack_bits = 0;            // K1->K3 scratch packing (0: two words per record)
 
   FlowTable tab{};
   uint64_t nslots = 0;
@@ -40,7 +40,7 @@ struct tcbee_ctx {
   uint32_t* d_slot_scratch = nullptr;
   uint32_t* d_len_scratch = nullptr;
   uint64_t* d_count_part = nullptr;  // K3 mode 0 per-block partial bins [k3_g1max][kCountBins]
-  uint64_t* d_k3_region = nullptr;   // K3 mode 1 (tables with > kCountBins slots only)
+  uint32_t* d_k3_region = nullptr;   // K3 mode 1 (tables with > kCountBins slots only)
   uint32_t* d_k3_offs = nullptr;
   uint64_t* d_k3_lpart = nullptr;
   uint32_t k3_nb_max = 0, k3_g2 = 0;

@@ -114,7 +114,9 @@ struct CountArgs {
   uint64_t* cnt;
   uint64_t* part;            // mode 0: [g1][kCountBins] per-block packed bins
   // mode 1 (large tables; region == nullptr disables it)
-  uint64_t* region;          // per accepted frame: (claim, caplen), bucket-sorted per block
+  uint32_t* region;          // per accepted frame: claim within its bucket | caplen
+                             // << kBucketBits (0 when >= kRegLenEsc: added by a global
+                             // atomic instead), bucket-sorted per block
   uint32_t* offs;            // [g1s][nb_max + 1] bucket offsets inside each block's region
   uint32_t nb_max;           // buckets the context's table can need
   uint64_t* lpart;           // [S][nb * kBucket][2] partial pkts/bytes per claim
@@ -177,5 +179,9 @@ constexpr uint64_t kK3Gran = 16384;
 constexpr uint64_t kK3MaxPer = (1ull << 24) - kK3Gran;
 constexpr int kBucketBits = 12, kBucket = 1 << kBucketBits;  // claims per mode-1 bucket
 constexpr uint32_t kMaxBuckets = 4096;    // mode 1 up to 16M flows (hist + cursors: 32 KiB)
+// mode-1 region entry: caplens from kRegLenEsc up are stored as 0 and their bytes
+// added to the flow's counter by a global atomic (frames of >= 1 MiB: never on a
+// real capture, but the ABI allows them)
+constexpr uint32_t kRegLenEsc = (1u << (32 - kBucketBits)) - 1;
 
 }  // namespace tcbee

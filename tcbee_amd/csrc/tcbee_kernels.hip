@@ -1086,8 +1086,9 @@ __global__ void k_assign(RankArgs r) {
 //     scans the counts, then scatters (claim, caplen) into its own region of a
 //     scratch buffer, bucket by bucket; k_count_bucket then histograms one bucket
 //     (from every block's segment of it) in LDS per workgroup; the reduce maps
-//     claims to ids. Replaces per-record device atomics (~86 ps per record at
-//     1M flows) with ~36 B of streaming traffic per record.
+//     claims to ids. Region entries are one word (claim within the bucket,
+//     20-bit caplen). Replaces per-record device atomics (~86 ps per record at
+//     1M flows) with ~28 B of streaming traffic per record.
 //  2  otherwise (or no scratch): per-record global atomics, wave-uniform flows
 //     aggregated first.
 constexpr uint64_t kBinByMask = (1ull << kBinPkShift) - 1;
@@ -1179,10 +1180,11 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
                               uint32_t* hist, uint32_t* cur, uint32_t* s_w) {
   const uint32_t tid = threadIdx.x;
   const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);
-  // (these ~nb hot LDS counters cost ~0.9 ms per 125M records at 31 buckets —
-  //  4x slower per atomic than K3 mode 0's thousands of bins; replicating each
-  //  counter 8x by lane did not change it: the cost is not same-address
-  //  serialization)
+  // Cost at 125M records, 31 buckets (tools/k3_ablate.sh): claim stream 0.09 ms,
+  // histogram atomics ~0, id gather + out_id stores ~0.55 ms, scattered region
+  // stores ~0.45 ms. The stores' cost is their count and scatter, not their
+  // bytes (8 -> 4-B entries saved 0.16 ms); moving the id gather into the second
+  // pass did not help (tried)
   for (uint32_t b = tid; b < nb; b += kCountBlock) hist[b] = 0;
   if (tid == 0) hist[kMaxBuckets] = cur[kMaxBuckets] = 0;
   __syncthreads();
@@ -1247,7 +1249,12 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
     }
 #pragma unroll
     for (int k = 0; k < U; ++k)
-      if (s[k] != 0xFFFFFFFFu) c.region[lo + pos[k]] = (uint64_t)s[k] | ((uint64_t)len[k] << 32);
+      if (s[k] != 0xFFFFFFFFu)
+        c.region[lo + pos[k]] = (s[k] & (kBucket - 1u)) | ((len[k] < kRegLenEsc ? len[k] : 0u) << kBucketBits);
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      if (s[k] != 0xFFFFFFFFu && len[k] >= kRegLenEsc)
+        atomicAdd((unsigned long long*)&c.cnt[2ull * c.cmap[s[k]] + 1], (unsigned long long)len[k]);
   }
 }
 
@@ -1413,16 +1420,16 @@ __global__ __launch_bounds__(kCountBlock) void k_count_bucket(CountArgs c, uint3
     const uint32_t* o = c.offs + (uint64_t)q * (c.nb_max + 1);
     const uint64_t a0 = lo_q + o[j], a1 = lo_q + o[j + 1];
     for (uint64_t x = a0 + lane; x < a1; x += 256) {
-      uint64_t v[4];
+      uint32_t v[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        v[u] = x + 64u * u < a1 ? __builtin_nontemporal_load(&c.region[x + 64u * u]) : ~0ull;
+        v[u] = __builtin_nontemporal_load(&c.region[x + 64u * u < a1 ? x + 64u * u : x]);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if (v[u] == ~0ull) continue;
-        const uint32_t t = (uint32_t)v[u] & (kBucket - 1);
+        if (x + 64u * u >= a1) continue;
+        const uint32_t t = v[u] & (kBucket - 1);
         atomicAdd((unsigned long long*)&s_pk[t], 1ull);
-        atomicAdd((unsigned long long*)&s_by[t], (unsigned long long)(v[u] >> 32));
+        atomicAdd((unsigned long long*)&s_by[t], (unsigned long long)(v[u] >> kBucketBits));
       }
     }
   }

@@ -240,10 +240,11 @@ def test_k3_big_caplen_and_hot_flow(gpu, oracle, flows, nopack, monkeypatch):
     tr = mixed_trace(150_000, seed=101, n_flows=flows)
     rng = np.random.default_rng(5)
     big = rng.choice(tr.n, size=300, replace=False)
-    pad = 300_000
+    pad = 2_600_000
     arena = np.concatenate([tr.arena, np.zeros(pad, np.uint8)])
     ln = tr.caplen.copy()
-    # 16383+ overflows the packed K1->K3 caplen field; 65536+ leaves the LDS bins
+    # 16383+ overflows the packed K1->K3 caplen field; 65536+ leaves the LDS bins;
+    # 2^20-1+ leaves the 20-bit caplen of a K3 mode-1 region entry (flows=20000)
     ln[big] = rng.integers(16_000, pad, size=len(big)).astype(np.uint32)
     tr2 = Trace(arena, tr.offset, ln, tr.ts_ns)
     with tcbee_amd.PacketParser(max_frames=1 << 18, max_arena=1 << 27, max_flows=1 << 16) as p:
