@@ -29,6 +29,7 @@ for s in "$@"; do
     dist2)  step dist2 600 env TCBEE_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --frames 20000000 --steps 5 --warmup 2 ;;
     sq)     step sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS --output-format csv -d gpurun_out/sq -o run -- python tools/k1_sweep.py --rounds 1 --iters 2 --fpl 2 --workloads imix10k ;;
     prof)   step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --no-cpu --no-extra --sample-check ;;
+    c4prof) step c4prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/c4prof -o run --output-format csv -- python bench.py --config4 --virtual-world 8 --steps 5 --warmup 1 --no-cpu --no-extra --sample-check ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
 done

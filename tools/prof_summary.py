@@ -37,7 +37,7 @@ def main():
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
         lines += ["Command: `rocprofv3 --kernel-trace --stats -- python bench.py --steps 10 "
-                  "--no-cpu --no-extra` (config 3: 100M IMIX frames, 10k flows).", "",
+                  "--no-cpu --no-extra --sample-check` (config 3: 100M IMIX frames, 10k flows).", "",
                   "| kernel | calls | avg us | total % |", "|---|---|---|---|"]
         for r in csv.DictReader(open(stats)):
             lines.append(f"| `{r['Name'][:70]}` | {r['Calls']} | "
@@ -76,6 +76,20 @@ def main():
                 for r in rd:
                     if "tcbee" in r["Kernel_Name"]:
                         wr.writerow([r[c] for c in cols])
+    c4 = os.path.join(OUT, "c4prof", "run_kernel_stats.csv")
+    if os.path.exists(c4):
+        shutil.copy(c4, os.path.join(PROF, f"{tag}_config4_kernel_stats.csv"))
+        lines += ["## config 4, one GPU's share", "",
+                  "Command: `rocprofv3 --kernel-trace --stats -- python bench.py --config4 "
+                  "--virtual-world 8 --steps 5 --warmup 1 --no-cpu --no-extra --sample-check` "
+                  "(rank 0's flow-hash shard of 1B IMIX frames / 8 GPUs: ~125M frames, "
+                  "~125k flows; K3 in its bucketed mode).", "",
+                  "| kernel | calls | avg us | total % |", "|---|---|---|---|"]
+        for r in csv.DictReader(open(c4)):
+            if "tcbee" in r["Name"]:
+                lines.append(f"| `{r['Name'][:70]}` | {r['Calls']} | "
+                             f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} |")
+        lines.append("")
     bench_log = os.path.join(OUT, "bench.log")
     if os.path.exists(bench_log):
         for ln in open(bench_log):
