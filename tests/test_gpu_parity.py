@@ -184,6 +184,39 @@ def test_device_path_matches_host_path(parser, oracle):
     assert dict(zip(["ingress", "egress", "handled", "dropped"], map(int, c))) == ctr
 
 
+def test_arena_beyond_4GiB(parser, oracle):
+    """Frames straddling and beyond the 4 GiB offset of a 4.3 GB device arena, the
+    last frame ending exactly at arena_len: 64-bit offsets all the way through."""
+    import torch
+    from tracegen import mixed_trace
+    tr = mixed_trace(40_000, seed=44, n_flows=700)
+    base = (1 << 32) - 777  # the trace crosses the 4 GiB line
+    alen = base + len(tr.arena)
+    n = tr.n
+    d_arena = torch.zeros(alen + 64, dtype=torch.uint8, device="cuda")
+    d_arena[base:alen] = torch.from_numpy(tr.arena).cuda()
+    d_off = torch.from_numpy((tr.offset + np.uint64(base)).view(np.int64)).cuda()
+    d_len = torch.from_numpy(tr.caplen.view(np.int32)).cuda()
+    d_ts = torch.from_numpy(tr.ts_ns.view(np.int64)).cuda()
+    d_rec = torch.empty(n * 74 + 16, dtype=torch.uint8, device="cuda")
+    d_hash = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_id = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_n = torch.zeros(1, dtype=torch.int64, device="cuda")
+    d_ctr = torch.zeros(4, dtype=torch.int64, device="cuda")
+    parser.reset_flows()
+    parser.parse_device(d_arena, alen, d_off, d_len, d_ts, n, d_rec, n, d_hash, d_id, d_n, d_ctr)
+    parser.sync()
+    k = int(d_n.item())
+    rec, fh, fi, ctr, table = oracle.parse(tr)
+    assert k == len(rec)
+    assert np.array_equal(d_rec[: k * 74].cpu().numpy().reshape(k, 74), rec)
+    assert np.array_equal(d_hash[:k].cpu().numpy().view(np.uint32), fh)
+    assert np.array_equal(d_id[:k].cpu().numpy().view(np.uint32), fi)
+    assert np.array_equal(parser.flows(), table)
+    del d_arena
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("fpl", ["1", "2", "4"])
 def test_tile_shape_determinism(gpu, oracle, fpl, monkeypatch):
     """Same trace, different frames-per-lane tilings -> identical outputs."""
