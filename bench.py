@@ -134,7 +134,8 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
                                         max_arena=0, max_flows=world * xcap)
         fm = FlowMerge(p, merged, xcap, n_global if flowhash else world * n, nbuf=nbuf)
         fm.gidx = gidx
-        om = OverlappedMerge(fm, nbuf=nbuf) if overlap else None
+        om = (OverlappedMerge(fm, nbuf=nbuf, timing=os.environ.get("TCBEE_BENCH_XTIME", "1") != "0")
+              if overlap else None)
     count = [0]
 
     def step():
@@ -161,6 +162,8 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
         step()
     torch.cuda.synchronize()
     p.profile(True)
+    if om is not None:
+        om.spans.clear()
     if multi:
         dist.barrier()
     torch.cuda.synchronize()
@@ -185,6 +188,12 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
              "pkts_total": int(flows["pkts"].sum())}
     if multi:
         check["ingress_global"] = int(last["ctr"][0].item())
+        if om is not None:
+            # side-stream span of one step's exchange (RCCL all-gather of the tables,
+            # merge, id remap, counter all-reduce), overlapping the next parse
+            xm = om.exchange_ms()
+            check["exchange_ms"] = round(xm, 4) if xm is not None else None
+            check["exchange_entries_per_rank"] = xcap
     if flowhash:
         check["frames_local"] = n
         if rank == 0:

@@ -1589,20 +1589,29 @@ __global__ void k_merge_finish(MergeArgs g) {
 }
 
 // ids[p] = map[ids[p]] (N>1 local -> global flow ids). The first kRemapLds map
-// entries are staged in LDS (a rank's local ids are dense from 0); the ids stream
+// entries are staged in LDS as u16 (a rank's local ids are dense from 0; a global
+// id >= 0xFFFF is looked up in HBM instead), 32 KiB per workgroup, so the remap
+// that overlaps the next step's K1 takes few of K1's LDS slots; the ids stream
 // through as 16-B non-temporal vectors, 4 per thread in flight.
 constexpr uint32_t kRemapLds = 16384;
 constexpr int kRemapBlock = 512;
 __global__ __launch_bounds__(kRemapBlock) void k_remap(uint32_t* ids, uint64_t n_max,
                                                        const uint64_t* n_dev, const uint32_t* map,
                                                        uint64_t map_len) {
-  __shared__ uint32_t s_map[kRemapLds];
+  __shared__ uint16_t s_map[kRemapLds];
   const uint64_t n = n_dev && *n_dev < n_max ? *n_dev : n_max;
   const uint32_t m = map_len < kRemapLds ? (uint32_t)map_len : kRemapLds;
-  for (uint32_t j = threadIdx.x; j < m; j += kRemapBlock) s_map[j] = map[j];
+  for (uint32_t j = threadIdx.x; j < m; j += kRemapBlock) {
+    const uint32_t g = map[j];
+    s_map[j] = g < 0xFFFFu ? (uint16_t)g : (uint16_t)0xFFFFu;
+  }
   __syncthreads();
   auto tr = [&](uint32_t v) -> uint32_t {
-    return v < m ? s_map[v] : (v < map_len ? map[v] : 0xFFFFFFFFu);
+    if (v < m) {
+      const uint32_t g = s_map[v];
+      return g != 0xFFFFu ? g : map[v];
+    }
+    return v < map_len ? map[v] : 0xFFFFFFFFu;
   };
   const uint64_t t0 = blockIdx.x * (uint64_t)kRemapBlock + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * kRemapBlock;
@@ -1909,8 +1918,14 @@ hipError_t launch_merge(const MergeArgs& g, const RankArgs& r, hipStream_t s) {
 
 hipError_t launch_remap(uint32_t* ids, uint64_t n_max, const uint64_t* n_dev, const uint32_t* map,
                         uint64_t map_len, hipStream_t s) {
+  // up to 512 workgroups (TCBEE_REMAP_GRID: A/B; beside the next step's K1,
+  // 32..512 workgroups gave the same step time once the LDS map was u16)
+  static const uint64_t gmax = [] {
+    const char* e = getenv("TCBEE_REMAP_GRID");
+    return e ? (uint64_t)atoll(e) : 512ull;
+  }();
   const uint64_t want = (n_max + 4ull * kRemapBlock - 1) / (4ull * kRemapBlock);
-  hipLaunchKernelGGL(k_remap, dim3((unsigned)(want < 512 ? (want ? want : 1) : 512)),
+  hipLaunchKernelGGL(k_remap, dim3((unsigned)(want < gmax ? (want ? want : 1) : gmax)),
                      dim3(kRemapBlock), 0, s, ids, n_max, n_dev, map,
                      map_len);
   return hipGetLastError();

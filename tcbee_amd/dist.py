@@ -115,11 +115,22 @@ class OverlappedMerge:
     slot's previous exchange is done with them. Only the export (a snapshot of the
     local table) stays on the main stream, ahead of the next step's table reset."""
 
-    def __init__(self, fm: FlowMerge, nbuf: int = 2):
+    def __init__(self, fm: FlowMerge, nbuf: int = 2, timing: bool = False):
         assert len(fm.ent) >= nbuf
         self.fm, self.nbuf = fm, nbuf
         self.side = torch.cuda.Stream()
         self.done = [None] * nbuf
+        self.timing = timing
+        self.spans = []  # (start, done) event pairs of the side-stream exchanges
+
+    def exchange_ms(self) -> float | None:
+        """Mean side-stream duration of the exchanges submitted since spans was
+        last cleared (all-gather + merge + remap + all-reduce, while overlapping the
+        next parse); None without timing."""
+        if not self.spans:
+            return None
+        self.spans[-1][1].synchronize()
+        return sum(a.elapsed_time(b) for a, b in self.spans) / len(self.spans)
 
     def acquire(self, slot: int) -> None:
         if self.done[slot] is not None:
@@ -133,9 +144,15 @@ class OverlappedMerge:
         ready.record(main)
         with torch.cuda.stream(self.side):
             self.side.wait_event(ready)
+            start = None
+            if self.timing:
+                start = torch.cuda.Event(enable_timing=True)
+                start.record(self.side)
             self.fm.merge(slot, out_id, n_dev, n_max, stream=self.side.cuda_stream)
             if ctr is not None:
                 dist.all_reduce(ctr, group=self.fm.group)  # global INGRESS/HANDLED/DROPPED
-            done = torch.cuda.Event()
+            done = torch.cuda.Event(enable_timing=self.timing)
             done.record(self.side)
+        if start is not None:
+            self.spans.append((start, done))
         self.done[slot] = done

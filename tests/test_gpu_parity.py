@@ -324,6 +324,34 @@ def test_device_merge_matches_unsharded(gpu, oracle, cuts):
         assert np.array_equal(m.flows(), full[4])
 
 
+@pytest.mark.parametrize("map_len,big", [(1, False), (5000, False), (16384, True),
+                                         (40_000, True)])
+def test_remap_ids_paths(gpu, map_len, big):
+    """ids[p] = map[ids[p]]: map entries staged in LDS (u16, first 16384), global ids
+    >= 0xFFFF and ids past the LDS part looked up in HBM, ids >= map_len -> ~0;
+    unaligned start, ragged tail, and the count taken from the device word."""
+    import torch
+    rng = np.random.default_rng(map_len)
+    hi = (1 << 31) if big else 60_000
+    mp = rng.integers(0, hi, size=map_len, dtype=np.int64).astype(np.uint32)
+    if big:
+        mp[::7] = np.uint32(0xFFFF)  # the LDS sentinel value itself is a valid id
+    n = 1_000_003
+    ids = rng.integers(0, map_len + 3, size=n + 5, dtype=np.int64).astype(np.uint32)
+    d = torch.from_numpy(ids.view(np.int32).copy()).cuda()
+    d_map = torch.from_numpy(mp.view(np.int32).copy()).cuda()
+    n_dev = torch.tensor([n - 2], dtype=torch.int64, device="cuda")
+    sub = d[1:]  # 4-B offset: the scalar head before the 16-B vectors
+    tcbee_amd.parser.remap_ids_device(sub, n, n_dev, d_map, map_len)
+    torch.cuda.synchronize()
+    got = sub.cpu().numpy().view(np.uint32)
+    src = ids[1:]
+    k = n - 2
+    want = np.where(src[:k] < map_len, mp[np.minimum(src[:k], map_len - 1)], np.uint32(0xFFFFFFFF))
+    assert np.array_equal(got[:k], want)
+    assert np.array_equal(got[k:], src[k:])  # past *n_dev: untouched
+
+
 def test_flow_table_full_reports(gpu):
     from tracegen import mixed_trace
     tr = mixed_trace(50_000, seed=5, n_flows=5000)
