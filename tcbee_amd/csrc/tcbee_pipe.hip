@@ -27,6 +27,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
+#include <immintrin.h>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -154,6 +155,8 @@ struct tcbee_pipe {
   Pool* pool = nullptr;
   tcbee_pipe_stats st{};
   uint64_t prefetch = 48;  // header-window gather: frames ahead (TCBEE_PIPE_PF, 0 = off)
+  int nt_copy = 1;         // header-window gather: fixed-size 16-B loads + streaming
+                           // stores into the staging (TCBEE_PIPE_NT=0: memcpy)
 };
 
 namespace {
@@ -231,6 +234,8 @@ void stage(tcbee_pipe* p, const tcbee_frames* in, Slot& s) {
   const uint64_t lo = s.lo, n = s.hi - s.lo, W = p->cfg.window;
   if (W) {
     const uint64_t pf = p->prefetch;
+    // (16-B streaming stores need a 16-B aligned staging slot per frame)
+    const bool nt = p->nt_copy && W % 16 == 0 && ((uintptr_t)s.h_arena & 15u) == 0;
     p->pool->run([&](unsigned part, unsigned parts) {
       const uint64_t a = n * part / parts, b = n * (part + 1) / parts;
       for (uint64_t k = a; k < b; ++k) {
@@ -246,6 +251,17 @@ void stage(tcbee_pipe* p, const tcbee_frames* in, Slot& s) {
         }
         const uint32_t len = in->caplen[f];
         const uint64_t o = in->offset[f];
+        if (nt && o + W <= in->arena_len) {
+          // the whole window, whatever the caplen: the bytes past caplen are never
+          // read (the kernels take caplen from h_len), so no per-frame length
+          // branch; streaming stores skip the read-for-ownership of the staging line
+          const __m128i* src = reinterpret_cast<const __m128i*>(in->arena + o);
+          __m128i* dst = reinterpret_cast<__m128i*>(s.h_arena + k * W);
+          for (uint64_t c = 0; c < W / 16; ++c) _mm_stream_si128(dst + c, _mm_loadu_si128(src + c));
+          s.h_len[k] = len;
+          s.h_ts[k] = in->ts_ns[f];
+          continue;
+        }
         const uint64_t want = len < W ? len : W;
         uint64_t cp = want;
         if (o >= in->arena_len) cp = 0;
@@ -255,6 +271,7 @@ void stage(tcbee_pipe* p, const tcbee_frames* in, Slot& s) {
         s.h_len[k] = len;
         s.h_ts[k] = in->ts_ns[f];
       }
+      if (nt) _mm_sfence();  // streaming stores visible before the H2D copy is issued
     });
     s.arena_used = n * W;
     return;
@@ -352,6 +369,7 @@ int tcbee_pipe_create(tcbee_pipe** out, int device, const tcbee_pipe_cfg* pc,
   p->device = device;
   p->cfg = c;
   if (const char* e = std::getenv("TCBEE_PIPE_PF")) p->prefetch = std::strtoull(e, nullptr, 10);
+  if (const char* e = std::getenv("TCBEE_PIPE_NT")) p->nt_copy = std::atoi(e);
   int rc = tcbee_ctx_create(&p->ctx, device, c.chunk_frames, 0, max_flows ? max_flows : 1 << 20);
   if (rc) return free_pipe(p), rc;
   void* cs = nullptr;

@@ -17,9 +17,14 @@ tr = tcbee_amd.synth_trace(n, sizes="imix", kind=1, n_flows=10_000)
 rec = np.empty((n, 74), np.uint8)
 ids = np.empty(n, np.uint32)
 pfs = [v for v in os.environ.get("PF_LIST", "").split(",") if v]
-for window, pf in ([(80, v) for v in pfs] if pfs else [(80, None), (0, None)]):
+nts = [v for v in os.environ.get("NT_LIST", "").split(",") if v]
+runs = ([(80, v, None) for v in pfs] + [(80, None, v) for v in nts]) or [(80, None, None),
+                                                                       (0, None, None)]
+for window, pf, nt in runs:
     if pf is not None:
         os.environ["TCBEE_PIPE_PF"] = pf
+    if nt is not None:
+        os.environ["TCBEE_PIPE_NT"] = nt
     with Pipeline(device=0, chunk_frames=1 << 20, window=window, depth=4, threads=16,
                   chunk_bytes=(1 << 29), max_flows=40_000) as p:
         p.run(tr, out_rec=rec, out_id=ids)
@@ -29,4 +34,4 @@ for window, pf in ([(80, v) for v in pfs] if pfs else [(80, None), (0, None)]):
             t0 = time.perf_counter()
             p.run(tr, out_rec=rec, out_id=ids)
             ts.append(time.perf_counter() - t0)
-    print(root, "window", window, "pf", pf, "Mpkt/s", round(n / float(np.median(ts)) / 1e6, 1), flush=True)
+    print(root, "window", window, "pf", pf, "nt", nt, "Mpkt/s", round(n / float(np.median(ts)) / 1e6, 1), flush=True)
