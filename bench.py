@@ -121,9 +121,14 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     # flow-hash shards hold ~n_flows/world flows each; the exchange carries `xcap`
     # entries per rank (checked against the real count after the run)
     flows_here = -(-n_flows // sw) if flowhash else n_flows
-    cap = max(4 * flows_here, 1 << 12)
-    # (a synthetic trace has at most n_flows flows; the exchange is sized to that, not
-    # to the 4x-headroom table)
+    # table sized for the flows the trace can hold (>= 2x slots, power of two): a
+    # contiguous shard sees at most n_flows, a flow-hash shard n_flows / N plus a
+    # few standard deviations of the hash split (the table accepts more anyway, up
+    # to its slot count; `status` would report a full one)
+    cap = flows_here + (8 * int(flows_here ** 0.5) + 64 if flowhash and sw > 1 else 0)
+    cap = max(cap, 1 << 12)
+    # (the exchange carries up to xcap entries per rank: a quarter more than the
+    # shard's expected flows)
     xcap = max(int(1.25 * flows_here) + 4096, 1 << 12)
     p = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=n, max_arena=0,
                                max_flows=cap)
@@ -337,7 +342,15 @@ def cpu_baseline(sizes, kind, n_flows, seed, seconds, threads, sample_n=2_000_00
     return out, tr.n
 
 
-def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=5, threads=16):
+def host_cores() -> int:
+    """CPUs this process may run on (what `nproc` prints)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=5, threads=None):
     """End-to-end rates from host memory: frames in pageable host RAM -> records +
     flow ids back in pageable host RAM (H2D and D2H inside the timed region).
       pipe_window80: tcbee_pipe, header-window staging (80 B/frame shipped)
@@ -347,6 +360,7 @@ def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=5, threads=16):
 
     import tcbee_amd
     from tcbee_amd.pipeline import Pipeline
+    threads = threads or host_cores()
     tr = tcbee_amd.synth_trace(n, sizes=sizes, kind=kind, n_flows=n_flows, seed=seed)
     rec = np.empty((n, 74), np.uint8)
     ids = np.empty(n, np.uint32)
@@ -368,7 +382,7 @@ def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=5, threads=16):
     m = 4_000_000
     sub = tr.slice(0, m)
     with tcbee_amd.PacketParser(max_frames=m, max_arena=len(sub.arena),
-                                max_flows=max(4 * n_flows, 1 << 12)) as p:
+                                max_flows=max(n_flows, 1 << 12)) as p:
         p.parse(sub)
         t0 = time.perf_counter()
         for _ in range(3):
@@ -379,7 +393,7 @@ def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=5, threads=16):
     return out
 
 
-def config5_replay(seed, n=1_000_000, n_flows=4, threads=16):
+def config5_replay(seed, n=1_000_000, n_flows=4, threads=None):
     """Config 5 of BASELINE.json: a trace file replayed end to end — classic pcap
     (tmpfs) -> tcbee_pipe (H2D, K1-K3, D2H) -> xdp.tcp -> the tcbee-process stage
     into SQLite (records pre-grouped by the GPU's flow ids) -> metrics.json. Each
@@ -399,6 +413,7 @@ def config5_replay(seed, n=1_000_000, n_flows=4, threads=16):
     tr = tcbee_amd.synth_trace(n, sizes="64", kind=1 if n_flows > 1 else 0, n_flows=n_flows,
                                seed=seed)
     d = tempfile.mkdtemp(prefix="tcbee_c5_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    threads = threads or host_cores()
     out = {"frames": n, "flows": n_flows, "frame_bytes": 64, "threads": threads}
     try:
         pcap = os.path.join(d, "trace.pcap")
@@ -463,9 +478,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip config-2 and e2e legs")
     ap.add_argument("--e2e-frames", type=int, default=20_000_000)
-    ap.add_argument("--shard", default="contig", choices=["contig", "flowhash"],
-                    help="N>1 partition: contiguous frame ranges (default) or flow-hash "
-                         "shards of one global trace of frames x N (the NIC-RSS view)")
+    ap.add_argument("--shard", default=None, choices=["contig", "flowhash"],
+                    help="partition of one global trace of frames x N: flow-hash shards "
+                         "(the NIC-RSS view, north_star's partition; default for N > 1) or "
+                         "contiguous frame ranges (every GPU sees every flow)")
     ap.add_argument("--config4", action="store_true",
                     help="config 4 of BASELINE.json: 125M IMIX frames per GPU, 1M flows, "
                          "flow-hash shards")
@@ -480,6 +496,10 @@ def main():
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.shard is None:
+        # N = 1: one shard either way (the whole trace); the contiguous build keeps
+        # the full bit-exact check of every record
+        args.shard = "flowhash" if world > 1 or args.virtual_world > 1 else "contig"
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -571,12 +591,15 @@ def main():
                                        n=args.e2e_frames)
             out["config5_replay"] = config5_replay(args.seed)
         if not args.no_cpu and world == 1:
-            threads = min(16, os.cpu_count() or 1)
+            # every core this process may run on (= nproc; on the GPU box the job's
+            # CPU share, not the machine's logical CPU count)
+            threads = host_cores()
             res, sample_n = cpu_baseline(args.sizes, kind, args.flows, args.seed,
                                          args.cpu_seconds, threads)
             v, done, el = res[threads]
             out["cpu_baseline"] = {
                 "value": round(v, 2), "unit": "Mpkt/s", "cores": threads, "kind": "port",
+                "nproc": threads, "machine_cpus": os.cpu_count(),
                 "sample": (f"{sample_n} frames of the same workload, repeated {done // sample_n}x "
                            f"({el:.1f}s); oracle/tcbee_oracle.c orc_baseline_run = xdp_hook + "
                            "per-thread FLOWS(100) + bincode serialize"),

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define TCBEE_ABI_VERSION 1
+#define TCBEE_ABI_VERSION 2
 
 /* ---- record / key layout constants (DESIGN.md "Data layout") ------------ */
 #define TCBEE_RECORD_BYTES   74  /* tcp_packet.rs:42 ENTRY_SIZE            */
@@ -47,6 +47,7 @@ extern "C" {
 #define TCBEE_KEY_BYTES      40  /* IpTuple + 2 zero bytes (hash/table key) */
 #define TCBEE_MAX_HDR_BYTES  74  /* eth 14 + ipv6 40 + tcp 20              */
 #define TCBEE_REF_MAX_FLOWS 100  /* config.rs:19 MAX_FLOWS                  */
+#define TCBEE_MAX_TABLE_FLOWS (1ull << 24) /* tcbee_ctx_create max_flows limit */
 
 /* ---- error codes --------------------------------------------------------- */
 #define TCBEE_OK                  0
@@ -60,6 +61,8 @@ extern "C" {
 #define TCBEE_EFORMAT            -8  /* malformed input file                    */
 #define TCBEE_ESPIN              -9  /* a bounded in-kernel wait timed out      */
 #define TCBEE_EDB               -10  /* SQLite statement failed (sink)          */
+#define TCBEE_ESHARD            -11  /* global-order export could not place a flow's
+                                        first record (see tcbee_flow_export_global_device) */
 
 /* ---- directions (which hook / which output file) ------------------------- */
 #define TCBEE_DIR_INGRESS 0  /* xdp_hook  -> xdp.tcp, counts INGRESS_EVENTS */
@@ -127,7 +130,10 @@ int         tcbee_device_count(int* n);
 /* ---- context --------------------------------------------------------------
  * max_frames: largest batch (frames) any parse call on this ctx will pass.
  * max_arena : largest arena (bytes) the HOST entry point will copy.
- * max_flows : flow-table capacity in distinct flows (table has >= 2x slots).
+ * max_flows : flow-table capacity in distinct flows (table has >= 2x slots,
+ *             a power of two, 64 B each); at most 2^24 (TCBEE_ECAPACITY above:
+ *             the table's 2 GiB bound). The table still accepts flows past
+ *             max_flows, up to its slot count (TCBEE_EFLOWFULL then).
  * device    : HIP device ordinal. */
 int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames,
                      uint64_t max_arena, uint64_t max_flows);
@@ -153,6 +159,22 @@ int tcbee_parse_batch_device(tcbee_ctx* ctx, const tcbee_frames* in_dev,
                              uint32_t* out_flow_hash, uint32_t* out_flow_id,
                              uint64_t* out_n_dev, tcbee_counters* ctr_dev,
                              void* stream);
+
+/* Extended outputs of a device-resident parse (ABI 2). */
+typedef struct tcbee_parse_ex {
+    /* [out_cap] u32: for each record written, the batch-local index of the frame
+     * it came from (NULL = not written). What a flow-hash shard of a real trace
+     * needs to place its flows in the global trace: rejected frames (non-TCP,
+     * runts, FILTER_PORT, xdp.rs:37-92) make record k != frame k. */
+    uint32_t* out_frame_index;
+    uint64_t  reserved[7];   /* zero */
+} tcbee_parse_ex;
+int tcbee_parse_batch_device_ex(tcbee_ctx* ctx, const tcbee_frames* in_dev,
+                                const tcbee_cfg* cfg,
+                                uint8_t* out_rec74, uint64_t out_cap,
+                                uint32_t* out_flow_hash, uint32_t* out_flow_id,
+                                uint64_t* out_n_dev, tcbee_counters* ctr_dev,
+                                const tcbee_parse_ex* ex, void* stream);
 
 /* Same, host buffers in and out (H2D of frames, D2H of records), synchronous.
  * out_n / ctr are host pointers; ctr is accumulated into. */
@@ -187,13 +209,47 @@ int tcbee_flow_export_device(tcbee_ctx* ctx, tcbee_flow_entry* out_dev, uint64_t
 int tcbee_flow_merge_device(tcbee_ctx* ctx, const tcbee_flow_entry* ent_dev,
                             uint64_t nseg, uint64_t stride, const uint64_t* seg_meta_dev,
                             uint64_t max_total_records, uint32_t* out_ids_dev, void* stream);
+/* Global-order export for a flow-hash shard (one rank's frames are a
+ * subsequence of one global trace). The context's table must
+ * hold the flows of ONE batch (reset before it, as a per-window recorder does).
+ * As tcbee_flow_export_device, but each entry's first_seen is the GLOBAL FRAME
+ * index of the flow's first record: frame_gidx_dev[rec_frame_dev[r]] for the
+ * flow's first record r of the batch (rec_frame_dev = that batch's
+ * tcbee_parse_ex.out_frame_index with out_cap >= its records), or
+ * frame_gidx_dev[r] when rec_frame_dev is NULL — allowed only if every one of
+ * the batch's n_frames frames was accepted, which the device checks.
+ * n_dev[1] = 0: the merge then rebases nothing, so flows of any partition merge
+ * in global first-seen order. A first record that cannot be placed exports
+ * first_seen ~0 and makes the next tcbee_ctx_status return TCBEE_ESHARD. */
+int tcbee_flow_export_global_device(tcbee_ctx* ctx, tcbee_flow_entry* out_dev, uint64_t cap,
+                                    uint64_t* n_dev, const uint32_t* rec_frame_dev,
+                                    const uint64_t* frame_gidx_dev, uint64_t n_frames,
+                                    uint64_t rec_frame_cap, void* stream);
+/* After merging global-order exports, first_seen of the merged table is a global
+ * FRAME index; the reference's is the global RECORD index (accepted frames
+ * before it). This rank's share: out_counts_dev[id] = number of this rank's
+ * records (first min(*n_rec_dev, n_rec_max); global frame of record k =
+ * frame_gidx_dev[rec_frame_dev ? rec_frame_dev[k] : k], ascending) whose global
+ * frame index is below merged flow id's first_seen, for ids < cap. Summed over
+ * ranks (an all-reduce) this is the global record index, which
+ * tcbee_flow_set_first_seen_device writes back. Asynchronous. */
+int tcbee_flow_records_before_device(tcbee_ctx* merged, const uint32_t* rec_frame_dev,
+                                     const uint64_t* frame_gidx_dev, const uint64_t* n_rec_dev,
+                                     uint64_t n_rec_max, uint64_t* out_counts_dev, uint64_t cap,
+                                     void* stream);
+int tcbee_flow_set_first_seen_device(tcbee_ctx* ctx, const uint64_t* fs_by_id_dev, uint64_t cap,
+                                     void* stream);
 /* ids[p] = map[ids[p]] for p < min(*n_dev, n_max) (n_dev may be NULL);
- * ids >= map_len or 0xFFFFFFFF become 0xFFFFFFFF: local ids -> merged ids. */
+ * ids >= map_len or 0xFFFFFFFF become 0xFFFFFFFF: local ids -> merged ids.
+ * No context: a NULL stream is HIP's null stream (callers that order the remap
+ * after work on their own stream must pass that stream). */
 int tcbee_remap_ids_device(uint32_t* ids_dev, uint64_t n_max, const uint64_t* n_dev,
                            const uint32_t* map_dev, uint64_t map_len, void* stream);
-/* The same, asynchronous on `stream` (NULL = the context's stream). */
+/* tcbee_flow_reset, asynchronous: applied by the next launch on the context
+ * (`stream` is not used). */
 int tcbee_flow_reset_device(tcbee_ctx* ctx, void* stream);
-/* Sticky status of the last batches: TCBEE_OK, TCBEE_EFLOWFULL or TCBEE_ESPIN.
+/* Sticky status of the last batches: TCBEE_OK, TCBEE_EFLOWFULL, TCBEE_ESPIN or
+ * TCBEE_ESHARD.
  * Synchronous; clears the status. */
 int tcbee_ctx_status(tcbee_ctx* ctx);
 

@@ -59,6 +59,17 @@ int tcbee_pcap_close(tcbee_pcap* p);
 int tcbee_pcap_write(const char* path, const tcbee_frames* in, int nanosecond,
                      uint32_t snaplen);
 
+/* ---- flow-hash partition (the NIC's RSS step for N GPUs) -----------------
+ * owner[i] = fold32(flow_hash64(key)) % world for every frame the hook can key
+ * (IPv4/TCP >= 54 B, IPv6/TCP >= 74 B; IpTuple at the fixed offsets of
+ * xdp.rs:37-127), so all frames of a flow reach one GPU and the per-GPU flow
+ * tables are disjoint; the same function places the device
+ * generator's config-4 shards. Frames without a key (non-TCP, runts) produce no
+ * record on any GPU and go round robin (i % world). FILTER_PORT is left to the
+ * owning GPU's hook. threads 0 = 1. */
+int tcbee_flowhash_owner(const tcbee_frames* in_host, uint32_t world, uint32_t threads,
+                         uint16_t* out_owner);
+
 /* ---- .tcp record files ----------------------------------------------------
  * Decoded TcpPacket (tcbee-process/src/bindings/tcp_packet.rs:8-28), the
  * struct tcbee-process builds from each 74-byte entry. */

@@ -415,6 +415,17 @@ uint64_t orc_flowtab_export(const orc_flowtab* ft, uint8_t* out, uint64_t cap) {
 }
 
 /* ---- batch: hook per frame, ring (= compacted output), FLOWS, counters --- */
+void orc_accept_mask(const uint8_t* arena, const uint64_t* offset, const uint32_t* caplen,
+                     uint64_t n, uint16_t filter_port, int direction, uint8_t* accept) {
+    for (uint64_t i = 0; i < n; ++i) {
+        orc_trace t;
+        orc_iptuple k;
+        const uint8_t* f = arena + offset[i];
+        accept[i] = (uint8_t)(direction ? orc_tc_hook(f, caplen[i], 0, filter_port, &t, &k)
+                                        : orc_xdp_hook(f, caplen[i], 0, filter_port, &t, &k));
+    }
+}
+
 uint64_t orc_parse_batch(const uint8_t* arena, const uint64_t* offset, const uint32_t* caplen,
                          const uint64_t* ts, uint64_t n, uint16_t filter_port, int direction,
                          uint8_t* out_rec, uint64_t out_cap, uint32_t* out_hash,

@@ -106,6 +106,10 @@ uint64_t     orc_flowtab_export(const orc_flowtab* ft, uint8_t* out64, uint64_t 
  * ft != NULL, per-record flow hash (low 32 bits of hash64 folded) / dense flow
  * id; record_base = global index of the first record (for first_seen).
  * Returns the number of records written. */
+/* accept[i] = 1 iff the hook emits a record for frame i (xdp.rs:37-92 /
+ * tc.rs:30-119): which frames of a partitioned trace become records. */
+void orc_accept_mask(const uint8_t* arena, const uint64_t* offset, const uint32_t* caplen,
+                     uint64_t n, uint16_t filter_port, int direction, uint8_t* accept);
 uint64_t orc_parse_batch(const uint8_t* arena, const uint64_t* offset,
                          const uint32_t* caplen, const uint64_t* ts, uint64_t n,
                          uint16_t filter_port, int direction,

@@ -31,6 +31,7 @@ EIO = -7
 EFORMAT = -8
 ESPIN = -9
 EDB = -10
+ESHARD = -11
 
 
 class TcbeeError(RuntimeError):
@@ -64,6 +65,10 @@ class FlowEntry(C.Structure):
                 ("bytes", C.c_uint64), ("first_seen", C.c_uint64)]
 
 
+class ParseEx(C.Structure):
+    _fields_ = [("out_frame_index", C.c_void_p), ("reserved", C.c_uint64 * 7)]
+
+
 class PipeCfg(C.Structure):
     _fields_ = [("chunk_frames", C.c_uint64), ("chunk_bytes", C.c_uint64),
                 ("window", C.c_uint32), ("depth", C.c_uint32), ("threads", C.c_uint32),
@@ -78,7 +83,7 @@ class PipeStats(C.Structure):
 PIPE_SINK_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64)
 
 assert C.sizeof(Cfg) == 8 and C.sizeof(Frames) == 48 and C.sizeof(PipeCfg) == 32
-assert C.sizeof(Counters) == 32 and C.sizeof(FlowEntry) == 64
+assert C.sizeof(Counters) == 32 and C.sizeof(FlowEntry) == 64 and C.sizeof(ParseEx) == 64
 
 # every symbol declared in include/tcbee_amd.h, with its ctypes signature
 _SIGS = {
@@ -93,6 +98,10 @@ _SIGS = {
     "tcbee_parse_batch_device": (C.c_int, [C.c_void_p, C.POINTER(Frames), C.POINTER(Cfg),
                                            C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_void_p]),
+    "tcbee_parse_batch_device_ex": (C.c_int, [C.c_void_p, C.POINTER(Frames), C.POINTER(Cfg),
+                                              C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                              C.c_void_p, C.c_void_p, C.POINTER(ParseEx),
+                                              C.c_void_p]),
     "tcbee_parse_batch": (C.c_int, [C.c_void_p, C.POINTER(Frames), C.POINTER(Cfg),
                                     C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                     C.POINTER(C.c_uint64), C.POINTER(Counters)]),
@@ -106,6 +115,14 @@ _SIGS = {
                                            C.c_void_p]),
     "tcbee_flow_merge_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
                                           C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "tcbee_flow_export_global_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64,
+                                                  C.c_void_p, C.c_void_p, C.c_void_p,
+                                                  C.c_uint64, C.c_uint64, C.c_void_p]),
+    "tcbee_flow_records_before_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p,
+                                                   C.c_void_p, C.c_uint64, C.c_void_p,
+                                                   C.c_uint64, C.c_void_p]),
+    "tcbee_flow_set_first_seen_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64,
+                                                   C.c_void_p]),
     "tcbee_remap_ids_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                          C.c_uint64, C.c_void_p]),
     "tcbee_ctx_profile": (C.c_int, [C.c_void_p, C.c_int]),

@@ -136,6 +136,7 @@ const char* tcbee_strerror(int code) {
     case TCBEE_EFORMAT: return "malformed input";
     case TCBEE_ESPIN: return "in-kernel wait timed out";
     case TCBEE_EDB: return "database statement failed";
+    case TCBEE_ESHARD: return "global-order export could not place a flow's first record";
     default: return "unknown error";
   }
 }
@@ -191,6 +192,9 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
                      uint64_t max_flows) {
   if (!out || max_frames == 0 || max_frames > (1ull << 40)) return TCBEE_EINVAL;
   *out = nullptr;
+  // 2^24 flows -> 2^25 slots = 2 GiB of table: K1's probe buffer resource and u32
+  // slot offsets, and K3's bucketed mode (kMaxBuckets x kBucket claims), end there
+  if (max_flows > kMaxTableFlows) return TCBEE_ECAPACITY;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return TCBEE_ENODEV;
   if (device < 0 || device >= ndev) return TCBEE_EINVAL;
@@ -223,9 +227,11 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   {
     // claims < nslots: log2(nslots) bits + 1 (so no packed word is all ones, the
     // no-flow mark); packed while at least 14 bits (caplen < 16383) remain
+    // (a standard Ethernet frame's 1518 B fits the 11 bits left at b = 21; longer
+    //  caplens saturate the field and go to the side array)
     uint32_t b = 1;
     while ((1ull << (b - 1)) < c->nslots) ++b;
-    c->pack_bits = b <= 18 ? b : 0;
+    c->pack_bits = b <= 21 ? b : 0;
     if (const char* e = std::getenv("TCBEE_TEST_NOPACK")) c->pack_bits = std::atoi(e) ? 0 : c->pack_bits;
   }
   c->max_tiles = (max_frames + tile_frames(1) - 1) / tile_frames(1);
@@ -316,11 +322,16 @@ int apply_pending_reset(tcbee_ctx* c, hipStream_t s) {
 }
 }  // namespace
 
-int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_cfg* cfg,
-                             uint8_t* out_rec74, uint64_t out_cap, uint32_t* out_flow_hash,
-                             uint32_t* out_flow_id, uint64_t* out_n_dev, tcbee_counters* ctr_dev,
-                             void* stream) {
+int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbee_cfg* cfg,
+                                uint8_t* out_rec74, uint64_t out_cap, uint32_t* out_flow_hash,
+                                uint32_t* out_flow_id, uint64_t* out_n_dev,
+                                tcbee_counters* ctr_dev, const tcbee_parse_ex* ex, void* stream) {
   if (!c || !in || !cfg) return TCBEE_EINVAL;
+  uint32_t* out_frame = ex ? ex->out_frame_index : nullptr;
+  if (ex)
+    for (uint64_t r : ex->reserved)
+      if (r) return TCBEE_EINVAL;
+  if (out_frame && in->n > 0xFFFFFFFFull) return TCBEE_EINVAL;  // u32 frame indices
   if (cfg->direction > 1) return TCBEE_EINVAL;
   if (in->n > c->max_frames) return TCBEE_ECAPACITY;
   if (in->n && (!in->arena || !in->offset || !in->caplen || !in->ts_ns)) return TCBEE_EINVAL;
@@ -367,6 +378,7 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     a.withhold_every = c->withhold_every;
     a.plain_walk = c->plain_walk;
     a.pack_bits = c->pack_bits;
+    a.out_frame = out_frame;
     const bool timed = c->profiling && c->ev_used < kMaxProfiled;
     if (timed) TRY_HIP(hipEventRecord(c->ev[2 * c->ev_used], s));
     TRY_HIP(launch_parse(a, fpl, flows, s, c->k1_variant));
@@ -426,6 +438,14 @@ int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_c
     TRY_HIP(launch_finalize(c->d_batch, c->d_persist, out_cap, out_n_dev, ctr_dev, cfg->direction, s));
   }
   return TCBEE_OK;
+}
+
+int tcbee_parse_batch_device(tcbee_ctx* c, const tcbee_frames* in, const tcbee_cfg* cfg,
+                             uint8_t* out_rec74, uint64_t out_cap, uint32_t* out_flow_hash,
+                             uint32_t* out_flow_id, uint64_t* out_n_dev, tcbee_counters* ctr_dev,
+                             void* stream) {
+  return tcbee_parse_batch_device_ex(c, in, cfg, out_rec74, out_cap, out_flow_hash, out_flow_id,
+                                     out_n_dev, ctr_dev, nullptr, stream);
 }
 
 int tcbee_parse_batch(tcbee_ctx* c, const tcbee_frames* in, const tcbee_cfg* cfg,
@@ -531,6 +551,52 @@ int tcbee_flow_export_device(tcbee_ctx* c, tcbee_flow_entry* out_dev, uint64_t c
   return TCBEE_OK;
 }
 
+int tcbee_flow_export_global_device(tcbee_ctx* c, tcbee_flow_entry* out_dev, uint64_t cap,
+                                    uint64_t* n_dev, const uint32_t* rec_frame_dev,
+                                    const uint64_t* frame_gidx_dev, uint64_t n_frames,
+                                    uint64_t rec_frame_cap, void* stream) {
+  if (!c || (cap && !out_dev) || (n_frames && !frame_gidx_dev)) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (int rc = apply_pending_reset(c, s)) return rc;
+  GlobalExportArgs g{};
+  g.tab = c->tab;
+  g.out = reinterpret_cast<uint64_t*>(out_dev);
+  g.cap = cap;
+  g.persist = c->d_persist;
+  g.batch = c->d_batch;
+  g.n_out = n_dev;
+  g.rec_frame = rec_frame_dev;
+  g.frame_gidx = frame_gidx_dev;
+  g.n_frames = n_frames;
+  g.out_cap = rec_frame_dev ? rec_frame_cap : ~0ull;
+  TRY_HIP(launch_export_global(g, s));
+  return TCBEE_OK;
+}
+
+int tcbee_flow_records_before_device(tcbee_ctx* c, const uint32_t* rec_frame_dev,
+                                     const uint64_t* frame_gidx_dev, const uint64_t* n_rec_dev,
+                                     uint64_t n_rec_max, uint64_t* out_counts_dev, uint64_t cap,
+                                     void* stream) {
+  if (!c || (cap && !out_counts_dev) || (n_rec_max && !frame_gidx_dev)) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (int rc = apply_pending_reset(c, s)) return rc;
+  TRY_HIP(launch_records_before(c->tab, rec_frame_dev, frame_gidx_dev, n_rec_dev, n_rec_max,
+                                out_counts_dev, cap, s));
+  return TCBEE_OK;
+}
+
+int tcbee_flow_set_first_seen_device(tcbee_ctx* c, const uint64_t* fs_by_id_dev, uint64_t cap,
+                                     void* stream) {
+  if (!c || (cap && !fs_by_id_dev)) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (int rc = apply_pending_reset(c, s)) return rc;
+  TRY_HIP(launch_set_first_seen(c->tab, fs_by_id_dev, cap, s));
+  return TCBEE_OK;
+}
+
 int tcbee_flow_merge_device(tcbee_ctx* c, const tcbee_flow_entry* ent_dev, uint64_t nseg,
                             uint64_t stride, const uint64_t* seg_meta_dev,
                             uint64_t max_total_records, uint32_t* out_ids_dev, void* stream) {
@@ -609,6 +675,7 @@ int tcbee_ctx_status(tcbee_ctx* c) {
     return TCBEE_EDEVICE;
   if (p.status & kStSpin) return TCBEE_ESPIN;
   if (p.status & kStFlowFull) return TCBEE_EFLOWFULL;
+  if (p.status & kStShard) return TCBEE_ESHARD;
   return TCBEE_OK;
 }
 

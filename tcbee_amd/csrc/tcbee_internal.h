@@ -8,7 +8,10 @@
 namespace tcbee {
 
 // Status bits (sticky, in PersistState::status)
-constexpr uint32_t kStFlowFull = 1u, kStSpin = 2u;
+//   kStShard: a global-order export (tcbee_flow_export_global_device) found a flow
+//   whose first record it cannot place (outside the last batch, past out_cap, or
+//   rejected frames without a record -> frame map)
+constexpr uint32_t kStFlowFull = 1u, kStSpin = 2u, kStShard = 4u;
 
 // Flow table in HBM, open addressing, linear probing, power-of-two slots.
 //  meta[s*8 + 0] tag word: 0 empty, 1 busy, else hash_tag32(h) | claim << 32,
@@ -78,6 +81,7 @@ struct ParseArgs {
   uint32_t withhold_every;  // test hook (TCBEE_TEST_WITHHOLD): 0 in production
   uint32_t plain_walk;      // probe steps past foreign slots with plain loads (kPlainWalk)
   uint32_t pack_bits;       // != 0: acc_flow = claim | min(caplen, lmax) << pack_bits
+  uint32_t* out_frame;      // optional: batch-local frame index of record p (p < out_cap)
 };
 constexpr uint32_t kPlainWalk = 8;
 
@@ -140,6 +144,30 @@ struct MergeArgs {
 };
 hipError_t launch_export(FlowTable t, uint64_t* out, uint64_t cap, const PersistState* p,
                          uint64_t* n_out, hipStream_t s);
+// Global-order export of a table built by ONE batch (flow-hash shards): entry
+// first_seen = frame_gidx[rec_frame[local record]] (rec_frame NULL: record k is
+// frame k, checked against n_frames); n_out[1] = 0 (nothing to rebase).
+struct GlobalExportArgs {
+  FlowTable tab;
+  uint64_t* out;
+  uint64_t cap;
+  PersistState* persist;
+  const BatchState* batch;
+  uint64_t* n_out;
+  const uint32_t* rec_frame;
+  const uint64_t* frame_gidx;
+  uint64_t n_frames;
+  uint64_t out_cap;  // records of the batch that have a rec_frame entry
+};
+hipError_t launch_export_global(const GlobalExportArgs& g, hipStream_t s);
+// Merged table (first_seen = global frame index): out[id] = number of this
+// rank's records whose global frame index is below the flow's first_seen.
+hipError_t launch_records_before(FlowTable t, const uint32_t* rec_frame,
+                                 const uint64_t* frame_gidx, const uint64_t* n_rec,
+                                 uint64_t n_rec_max, uint64_t* out, uint64_t cap, hipStream_t s);
+// first_seen of flow id := fs_by_id[id] (ids < cap)
+hipError_t launch_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t cap,
+                                 hipStream_t s);
 hipError_t launch_merge(const MergeArgs& g, const RankArgs& r, hipStream_t s);
 hipError_t launch_remap(uint32_t* ids, uint64_t n_max, const uint64_t* n_dev, const uint32_t* map,
                         uint64_t map_len, hipStream_t s);
@@ -179,6 +207,7 @@ constexpr uint64_t kK3Gran = 16384;
 constexpr uint64_t kK3MaxPer = (1ull << 24) - kK3Gran;
 constexpr int kBucketBits = 12, kBucket = 1 << kBucketBits;  // claims per mode-1 bucket
 constexpr uint32_t kMaxBuckets = 4096;    // mode 1 up to 16M flows (hist + cursors: 32 KiB)
+constexpr uint64_t kMaxTableFlows = 1ull << 24;  // tcbee_ctx_create's max_flows limit
 // mode-1 region entry: caplens from kRegLenEsc up are stored as 0 and their bytes
 // added to the flow's counter by a global atomic (frames of >= 1 MiB: never on a
 // real capture, but the ABI allows them)

@@ -626,9 +626,10 @@ void k_parse(ParseArgs a) {
   if (FLOWS) {
     // phase B: hash, then issue the first probe's slot-line loads of every frame
     uint64_t h[FPL], W[FPL][7];
+    // num_records = table bytes (<= 2 GiB: tcbee_ctx_create caps max_flows at
+    // kMaxTableFlows, so slot offsets fit u32); the bits are read as unsigned
     const __amdgpu_buffer_rsrc_t meta_rs = __builtin_amdgcn_make_buffer_rsrc(
-        a.tab.meta, 0, (int)((a.tab.mask + 1) * 64u > 0x7FFFFFFFull ? 0x7FFFFFFF : (a.tab.mask + 1) * 64u),
-        0x00020000);
+        a.tab.meta, 0, (int)(uint32_t)((a.tab.mask + 1) * 64u), 0x00020000);
     bool uni[FPL], want[FPL];
     uint32_t leader[FPL];
 #pragma unroll
@@ -779,6 +780,8 @@ void k_parse(ParseArgs a) {
     const uint64_t p = excl + rank[f];
     if (acc[f] && !(ABL & 16)) {
       if (a.out_hash && p < a.out_cap) st_stream<NT>(a.out_hash + p, hsh[f]);
+      // record -> frame map (flow-hash shards of traces with rejected frames)
+      if (a.out_frame && p < a.out_cap) st_stream<NT>(a.out_frame + p, (uint32_t)(i0 + (uint64_t)f * kBlock + tid));
       if (FLOWS) {
         if (a.pack_bits) {
           // (claim, caplen) in one word; a caplen that does not fit saturates the
@@ -955,10 +958,15 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
     const uint64_t s = r.new_list[j];
     const uint64_t local = r.tab.meta[8 * s + 6] - base;
     const uint64_t w = local >> 5;
-    const uint32_t below = __hip_atomic_load(&r.bitmap[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
-                           ((1u << (local & 31)) - 1u);
-    r.tab.meta[8 * s + 7] = fbase + r.wprefix[w] + __popc(below) + 1;
-    r.tab.cmap[fbase + j] = (uint32_t)(fbase + r.wprefix[w] + __popc(below));
+    uint64_t id = fbase + n_new - 1;  // first_seen outside the batch (an invalid merge
+                                      // input, flagged by its exporter): no bitmap read
+    if (w < lim) {
+      const uint32_t below = __hip_atomic_load(&r.bitmap[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+                             ((1u << (local & 31)) - 1u);
+      id = fbase + r.wprefix[w] + __popc(below);
+    }
+    r.tab.meta[8 * s + 7] = id + 1;
+    r.tab.cmap[fbase + j] = (uint32_t)id;
   }
 }
 
@@ -1056,6 +1064,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_blocks(RankArgs r) {
 
 __global__ void k_assign(RankArgs r) {
   const uint64_t n_new = r.batch->n_new;
+  const uint64_t lim = rank_words(r);
   const uint64_t base = r.persist->rec_base;
   const uint64_t fbase = r.persist->flow_count;
   for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n_new;
@@ -1063,8 +1072,11 @@ __global__ void k_assign(RankArgs r) {
     const uint64_t s = r.new_list[j];
     const uint64_t local = r.tab.meta[8 * s + 6] - base;
     const uint64_t w = local >> 5;
-    const uint32_t below = r.bitmap[w] & ((1u << (local & 31)) - 1u);
-    const uint64_t id = fbase + r.bprefix[w / kScanWordsPerBlock] + r.wprefix[w] + __popc(below);
+    uint64_t id = fbase + n_new - 1;  // first_seen outside the batch: see k_rank_small
+    if (w < lim) {
+      const uint32_t below = r.bitmap[w] & ((1u << (local & 31)) - 1u);
+      id = fbase + r.bprefix[w / kScanWordsPerBlock] + r.wprefix[w] + __popc(below);
+    }
     r.tab.meta[8 * s + 7] = id + 1;
     r.tab.cmap[fbase + j] = (uint32_t)id;
   }
@@ -1534,6 +1546,86 @@ __global__ void k_export(FlowTable t, uint64_t* out, uint64_t cap, const Persist
   }
 }
 
+// Global-order export (flow-hash shards). The table holds the flows of ONE batch
+// (records [rec_base - n_acc, rec_base) of the context); a flow's first record r
+// is mapped to its frame (rec_frame[r], or r itself when every frame of the batch
+// was accepted) and that frame to its position in the global trace. A first
+// record that cannot be placed flags kStShard and exports first_seen ~0.
+__global__ void k_export_global(GlobalExportArgs g) {
+  const uint64_t nslots = g.tab.mask + 1;
+  const uint64_t hi = g.persist->rec_base, nacc = g.batch->n_acc, lo = hi - nacc;
+  const bool identity = g.rec_frame == nullptr;
+  const bool bad_batch = identity && nacc != g.n_frames;
+  bool bad = false;
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < nslots;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t* m = g.tab.meta + 8 * s;
+    if (m[0] < 2 || m[7] == 0) continue;
+    const uint64_t id = m[7] - 1;
+    if (id >= g.cap) continue;
+    uint64_t* e = g.out + 8 * id;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) e[j] = m[1 + j];
+    e[5] = g.tab.cnt[2 * id];
+    e[6] = g.tab.cnt[2 * id + 1];
+    const uint64_t fs = m[6];
+    uint64_t gfs = ~0ull;
+    if (fs >= lo && fs < hi && fs - lo < g.out_cap && !bad_batch) {
+      const uint64_t r = fs - lo;
+      const uint64_t fr = identity ? r : g.rec_frame[r];
+      if (fr < g.n_frames) gfs = g.frame_gidx[fr];
+    }
+    bad = bad || gfs == ~0ull;
+    e[7] = gfs;
+  }
+  if (__any(bad) && __lane_id() == 0) atomicOr(&g.persist->status, kStShard);
+  if (g.n_out && blockIdx.x == 0 && threadIdx.x == 0) {
+    g.n_out[0] = g.persist->flow_count < g.cap ? g.persist->flow_count : g.cap;
+    g.n_out[1] = 0;  // first_seen is already global: the merge rebases nothing
+    if (bad_batch) atomicOr(&g.persist->status, kStShard);
+  }
+}
+
+// Records of this rank below each merged flow's first frame: a binary search
+// over the rank's record stream, whose global frame indices ascend.
+__global__ void k_records_before(FlowTable t, const uint32_t* rec_frame,
+                                 const uint64_t* frame_gidx, const uint64_t* n_rec_dev,
+                                 uint64_t n_rec_max, uint64_t* out, uint64_t cap) {
+  const uint64_t nslots = t.mask + 1;
+  const uint64_t n = n_rec_dev && *n_rec_dev < n_rec_max ? *n_rec_dev : n_rec_max;
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < nslots;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t* m = t.meta + 8 * s;
+    if (m[0] < 2 || m[7] == 0) continue;
+    const uint64_t id = m[7] - 1;
+    if (id >= cap) continue;
+    const uint64_t G = m[6];
+    uint64_t lo = 0, len = n;  // first record whose global frame >= G
+    while (len > 0) {
+      const uint64_t half = len >> 1, mid = lo + half;
+      const uint64_t gm = frame_gidx[rec_frame ? rec_frame[mid] : mid];
+      if (gm < G) {
+        lo = mid + 1;
+        len -= half + 1;
+      } else {
+        len = half;
+      }
+    }
+    out[id] = lo;
+  }
+}
+
+__global__ void k_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t cap) {
+  const uint64_t nslots = t.mask + 1;
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < nslots;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t* m = t.meta + 8 * s;
+    if (m[0] < 2 || m[7] == 0) continue;
+    const uint64_t id = m[7] - 1;
+    if (id < cap) m[6] = fs_by_id[id];
+  }
+}
+
 // Inserts every valid entry of nseg segments (segment r = rank r's local table,
 // first_seen local to that rank) with first_seen rebased to the global record
 // index; per-slot counters summed. out_slot[e] = merged slot (or ~0).
@@ -1906,6 +1998,24 @@ hipError_t launch_export(FlowTable t, uint64_t* out, uint64_t cap, const Persist
   return hipGetLastError();
 }
 
+hipError_t launch_export_global(const GlobalExportArgs& g, hipStream_t s) {
+  hipLaunchKernelGGL(k_export_global, dim3(grid_for(g.tab.mask + 1)), dim3(kBlock), 0, s, g);
+  return hipGetLastError();
+}
+
+hipError_t launch_records_before(FlowTable t, const uint32_t* rec_frame, const uint64_t* frame_gidx,
+                                 const uint64_t* n_rec, uint64_t n_rec_max, uint64_t* out,
+                                 uint64_t cap, hipStream_t s) {
+  hipLaunchKernelGGL(k_records_before, dim3(grid_for(t.mask + 1)), dim3(kBlock), 0, s, t, rec_frame,
+                     frame_gidx, n_rec, n_rec_max, out, cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t cap, hipStream_t s) {
+  hipLaunchKernelGGL(k_set_first_seen, dim3(grid_for(t.mask + 1)), dim3(kBlock), 0, s, t, fs_by_id, cap);
+  return hipGetLastError();
+}
+
 hipError_t launch_merge(const MergeArgs& g, const RankArgs& r, hipStream_t s) {
   const unsigned grid = grid_for(g.nseg * g.stride);
   hipLaunchKernelGGL(k_merge_insert, dim3(grid), dim3(kBlock), 0, s, g);
@@ -1922,7 +2032,8 @@ hipError_t launch_remap(uint32_t* ids, uint64_t n_max, const uint64_t* n_dev, co
   // 32..512 workgroups gave the same step time once the LDS map was u16)
   static const uint64_t gmax = [] {
     const char* e = getenv("TCBEE_REMAP_GRID");
-    return e ? (uint64_t)atoll(e) : 512ull;
+    const long long v = e ? atoll(e) : 0;
+    return v > 0 ? (uint64_t)v : 512ull;  // unset, 0 or garbage: the default
   }();
   const uint64_t want = (n_max + 4ull * kRemapBlock - 1) / (4ull * kRemapBlock);
   hipLaunchKernelGGL(k_remap, dim3((unsigned)(want < gmax ? (want ? want : 1) : gmax)),

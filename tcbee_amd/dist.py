@@ -52,7 +52,18 @@ class FlowMerge:
 
     step(): export the local table (device), all-gather tables + {count, records}
     over RCCL, merge them on this GPU into `merged` (identical on every rank),
-    then rewrite this rank's record flow ids from local to global ids."""
+    then rewrite this rank's record flow ids from local to global ids.
+
+    Two partitions of one global frame stream:
+      contiguous ranges (gidx None): segment r's first_seen is local to rank r and
+        the merge rebases it by the records of ranks < r;
+      any other partition, e.g. flow-hash shards (gidx = global frame index of each
+        local frame, ascending): the export carries the global FRAME index of each
+        flow's first record (through the record -> frame map `rec_frame` when
+        frames were rejected), the merge ranks flows by it, and the merged
+        first_seen is turned back into the global RECORD index by one all-reduce
+        of per-rank record counts (tcbee_flow_records_before_device). Tables of
+        one step only: the local table is reset before every parse."""
 
     def __init__(self, local: "_parser.PacketParser", merged: "_parser.PacketParser",
                  cap: int, max_total_records: int, group=None, nbuf: int = 1):
@@ -68,33 +79,41 @@ class FlowMerge:
                     for _ in range(nbuf)]
         self.meta = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(nbuf)]
         self.ids = torch.empty(self.world * cap, dtype=torch.int32, device=dev)
-        # flow-hash shards (set by the caller): global frame index of each local frame
+        # non-contiguous partitions (set by the caller): global frame index of each
+        # local frame (device int64, ascending)
         self.gidx: torch.Tensor | None = None
+        self.fs_counts = torch.zeros(self.world * cap, dtype=torch.int64, device=dev)
 
-    def export(self, slot: int = 0, stream: int | None = None) -> None:
+    def export(self, slot: int = 0, stream: int | None = None, rec_frame=None,
+               rec_cap: int = 0) -> None:
         """Snapshot of the local table into export slot `slot` (before the next parse).
         Pass a non-NULL stream handle: NULL means the context's own stream.
-
-        With `gidx` set (flow-hash shards: a rank's frames are a subsequence of the
-        global stream, and its flows are its own), first_seen becomes the global
-        index of the flow's first record and the merge rebases nothing. That needs
-        record k == local frame k, i.e. every frame accepted (true for the synthetic
-        IPv4/TCP traces this mode is built for)."""
-        self.local.export_device(self.ent[slot], self.cap, self.meta[slot], stream=stream)
-        if self.gidx is not None:
-            ent, meta = self.ent[slot], self.meta[slot]
-            valid = torch.arange(self.cap, device=ent.device) < meta[0]
-            fs = ent[:, 7].clamp(0, self.gidx.numel() - 1)
-            ent[:, 7] = torch.where(valid, self.gidx[fs], ent[:, 7])
-            meta[1] = 0
+        With `gidx` set, first_seen becomes the global frame index of each flow's
+        first record: via rec_frame (the parse's out_frame, rec_cap entries) or,
+        without it, assuming every frame was accepted (checked on the device:
+        otherwise the local context's status reports TCBEE_ESHARD)."""
+        if self.gidx is None:
+            self.local.export_device(self.ent[slot], self.cap, self.meta[slot], stream=stream)
+        else:
+            self.local.export_global_device(self.ent[slot], self.cap, self.meta[slot],
+                                            self.gidx, self.gidx.numel(), rec_frame=rec_frame,
+                                            rec_frame_cap=rec_cap, stream=stream)
 
     def merge(self, slot: int, out_id: torch.Tensor | None, n_dev: torch.Tensor | None,
-              n_max: int, stream: int | None = None):
+              n_max: int, stream: int | None = None, rec_frame=None):
         """All-gather slot's tables (RCCL, current torch stream), merge them on this GPU
         and rewrite out_id from local to global ids, on `stream`."""
         all_ent, all_meta = gather_tables(self.ent[slot], self.meta[slot], self.group)
         self.merged.merge_device(all_ent, self.world, self.cap, all_meta, self.max_total,
                                  self.ids, stream=stream)
+        if self.gidx is not None:
+            # merged first_seen: global frame index -> global record index
+            mcap = self.world * self.cap
+            self.fs_counts.zero_()
+            self.merged.records_before_device(rec_frame, self.gidx, n_dev, n_max,
+                                              self.fs_counts, mcap, stream=stream)
+            dist.all_reduce(self.fs_counts, group=self.group)
+            self.merged.set_first_seen_device(self.fs_counts, mcap, stream=stream)
         if out_id is not None:
             lo = self.rank * self.cap
             _parser.remap_ids_device(out_id, n_max, n_dev, self.ids[lo:lo + self.cap],
@@ -102,10 +121,10 @@ class FlowMerge:
         return all_ent, all_meta
 
     def step(self, out_id: torch.Tensor | None, n_dev: torch.Tensor | None, n_max: int,
-             stream: int | None = None):
+             stream: int | None = None, rec_frame=None):
         """export + merge on one stream (the torch current stream must be `stream`)."""
-        self.export(0, stream=stream)
-        return self.merge(0, out_id, n_dev, n_max, stream=stream)
+        self.export(0, stream=stream, rec_frame=rec_frame, rec_cap=n_max)
+        return self.merge(0, out_id, n_dev, n_max, stream=stream, rec_frame=rec_frame)
 
 
 class OverlappedMerge:
@@ -137,9 +156,9 @@ class OverlappedMerge:
             torch.cuda.current_stream().wait_event(self.done[slot])
 
     def submit(self, slot: int, out_id: torch.Tensor | None, n_dev: torch.Tensor | None,
-               n_max: int, ctr: torch.Tensor | None = None) -> None:
+               n_max: int, ctr: torch.Tensor | None = None, rec_frame=None) -> None:
         main = torch.cuda.current_stream()
-        self.fm.export(slot, stream=main.cuda_stream)
+        self.fm.export(slot, stream=main.cuda_stream, rec_frame=rec_frame, rec_cap=n_max)
         ready = torch.cuda.Event()
         ready.record(main)
         with torch.cuda.stream(self.side):
@@ -148,7 +167,8 @@ class OverlappedMerge:
             if self.timing:
                 start = torch.cuda.Event(enable_timing=True)
                 start.record(self.side)
-            self.fm.merge(slot, out_id, n_dev, n_max, stream=self.side.cuda_stream)
+            self.fm.merge(slot, out_id, n_dev, n_max, stream=self.side.cuda_stream,
+                          rec_frame=rec_frame)
             if ctr is not None:
                 dist.all_reduce(ctr, group=self.fm.group)  # global INGRESS/HANDLED/DROPPED
             done = torch.cuda.Event(enable_timing=self.timing)

@@ -89,6 +89,7 @@ _SIGS = {
     "tcbee_tsdb_set_attribute": (cint, [vp, i64, cstr, cint, i64, dbl, cstr]),
     "tcbee_tsdb_delete_attribute": (cint, [vp, i64, cstr]),
     "tcbee_metrics_write": (cint, [cstr, C.POINTER(Counters), u64, u64]),
+    "tcbee_flowhash_owner": (cint, [C.POINTER(Frames), C.c_uint32, C.c_uint32, vp]),
 }
 HOST_EXPORTED = tuple(_SIGS)
 
@@ -175,6 +176,22 @@ class Pcap:
             self.close()
         except Exception:
             pass
+
+
+def flowhash_owner(trace: Trace, world: int, threads: int = 8) -> np.ndarray:
+    """GPU owning each frame under the flow-hash partition (tcbee_flowhash_owner:
+    the NIC-RSS step; frames the hook cannot key go round robin)."""
+    out = np.empty(max(trace.n, 1), dtype=np.uint16)
+    fr = _frames_of(trace)
+    _check(hlib().tcbee_flowhash_owner(C.byref(fr), world, threads, _ptr(out)),
+           "tcbee_flowhash_owner")
+    return out[:trace.n]
+
+
+def flowhash_shard(trace: Trace, world: int, rank: int, threads: int = 8):
+    """(rank's frames as a zero-copy Trace, their global frame indices)."""
+    gidx = np.nonzero(flowhash_owner(trace, world, threads) == rank)[0].astype(np.int64)
+    return trace.select(gidx), gidx
 
 
 def write_pcap(path: str, trace: Trace, nanosecond: bool = True, snaplen: int = 262144) -> None:

@@ -133,16 +133,24 @@ class PacketParser:
                      out_rec, out_cap: int, out_hash=None, out_id=None, out_n=None,
                      counters=None, filter_port: int = 0,
                      direction: int = _lib.DIR_INGRESS, flows: bool = True,
-                     stream: int | None = None) -> None:
+                     stream: int | None = None, out_frame=None) -> None:
         """Asynchronous parse of frames already in HBM (pointers or torch tensors).
 
-        out_n: device u64[1]; counters: device u64[4] (accumulated)."""
+        out_n: device u64[1]; counters: device u64[4] (accumulated); out_frame:
+        device u32[out_cap], the batch-local frame index of each record."""
         fr = _lib.Frames(_ptr(arena), arena_len, _ptr(offset), _ptr(caplen), _ptr(ts_ns), n)
         cfg = _lib.Cfg(filter_port, direction, 0, 0 if flows else _lib.F_NO_FLOWS)
-        _lib.check(_lib.lib().tcbee_parse_batch_device(
+        if out_frame is None:
+            _lib.check(_lib.lib().tcbee_parse_batch_device(
+                self._h, C.byref(fr), C.byref(cfg), _ptr(out_rec), C.c_uint64(out_cap),
+                _ptr(out_hash), _ptr(out_id), _ptr(out_n), _ptr(counters),
+                C.c_void_p(stream or 0)), "tcbee_parse_batch_device")
+            return
+        ex = _lib.ParseEx(_ptr(out_frame))
+        _lib.check(_lib.lib().tcbee_parse_batch_device_ex(
             self._h, C.byref(fr), C.byref(cfg), _ptr(out_rec), C.c_uint64(out_cap),
-            _ptr(out_hash), _ptr(out_id), _ptr(out_n), _ptr(counters),
-            C.c_void_p(stream or 0)), "tcbee_parse_batch_device")
+            _ptr(out_hash), _ptr(out_id), _ptr(out_n), _ptr(counters), C.byref(ex),
+            C.c_void_p(stream or 0)), "tcbee_parse_batch_device_ex")
 
     # -- measurement --------------------------------------------------------------
     def profile(self, enable: bool = True) -> None:
@@ -185,6 +193,31 @@ class PacketParser:
         _lib.check(_lib.lib().tcbee_flow_export_device(
             self._h, _ptr(out), C.c_uint64(cap), _ptr(meta), C.c_void_p(stream or 0)),
             "tcbee_flow_export_device")
+
+    def export_global_device(self, out, cap: int, meta, frame_gidx, n_frames: int,
+                             rec_frame=None, rec_frame_cap: int = 0,
+                             stream: int | None = None) -> None:
+        """As export_device, first_seen = global frame index of each flow's first
+        record (frame_gidx[rec_frame[r]], or frame_gidx[r] when every frame was
+        accepted); meta[1] = 0. The table must hold one batch's flows."""
+        _lib.check(_lib.lib().tcbee_flow_export_global_device(
+            self._h, _ptr(out), C.c_uint64(cap), _ptr(meta), _ptr(rec_frame), _ptr(frame_gidx),
+            C.c_uint64(n_frames), C.c_uint64(rec_frame_cap), C.c_void_p(stream or 0)),
+            "tcbee_flow_export_global_device")
+
+    def records_before_device(self, rec_frame, frame_gidx, n_rec_dev, n_rec_max: int,
+                              out_counts, cap: int, stream: int | None = None) -> None:
+        """out_counts[id] = this rank's records whose global frame index is below
+        merged flow id's first_seen (a global frame index)."""
+        _lib.check(_lib.lib().tcbee_flow_records_before_device(
+            self._h, _ptr(rec_frame), _ptr(frame_gidx), _ptr(n_rec_dev), C.c_uint64(n_rec_max),
+            _ptr(out_counts), C.c_uint64(cap), C.c_void_p(stream or 0)),
+            "tcbee_flow_records_before_device")
+
+    def set_first_seen_device(self, fs_by_id, cap: int, stream: int | None = None) -> None:
+        _lib.check(_lib.lib().tcbee_flow_set_first_seen_device(
+            self._h, _ptr(fs_by_id), C.c_uint64(cap), C.c_void_p(stream or 0)),
+            "tcbee_flow_set_first_seen_device")
 
     def merge_device(self, entries, nseg: int, stride: int, seg_meta, max_total_records: int,
                      out_ids, stream: int | None = None) -> None:
@@ -243,7 +276,12 @@ def gen_shard_scratch_words(n_global: int) -> int:
 
 def remap_ids_device(ids, n_max: int, n_dev, id_map, map_len: int,
                      stream: int | None = None) -> None:
-    """ids[p] = id_map[ids[p]] for p < min(*n_dev, n_max)."""
+    """ids[p] = id_map[ids[p]] for p < min(*n_dev, n_max). Without a stream the
+    remap goes on torch's current stream (the C ABI would read NULL as HIP's null
+    stream, which other streams do not wait for)."""
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream().cuda_stream
     _lib.check(_lib.lib().tcbee_remap_ids_device(
         _ptr(ids), C.c_uint64(n_max), _ptr(n_dev), _ptr(id_map), C.c_uint64(map_len),
         C.c_void_p(stream or 0)), "tcbee_remap_ids_device")

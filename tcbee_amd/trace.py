@@ -64,6 +64,12 @@ class Trace:
         return Trace(self.arena[a0:a1].copy(), off - np.uint64(a0), ln.copy(),
                      self.ts_ns[lo:hi].copy())
 
+    def select(self, idx: np.ndarray) -> "Trace":
+        """Frames idx (ascending), sharing this trace's arena (zero-copy: the
+        offsets still point into it) — one GPU's part of a partitioned trace."""
+        idx = np.asarray(idx, dtype=np.int64)
+        return Trace(self.arena, self.offset[idx], self.caplen[idx], self.ts_ns[idx])
+
     @staticmethod
     def from_frames(frames, ts_ns=None) -> "Trace":
         """Pack a list of byte strings back to back."""

@@ -40,21 +40,75 @@ def run(rank, world, port, n, cap, result_dir):
     dist.destroy_process_group()
 
 
-def run_gpu(rank, world, port, n, cap, result_dir, mode):
-    """N>1 choreography on the GPU: ranks share device 0 over gloo. mode "step":
-    FlowMerge.step on one stream; mode "overlap": OverlappedMerge over 3 steps of
-    the same shard (fresh table each step, output slots rotating), as bench.py;
-    mode "flowhash": the rank's flow-hash shard of a synthetic global trace of n
-    frames, built by the device generator, exchanged with global first_seen."""
+def run_flowhash(rank, world, port, n, cap, result_dir, filter_port):
+    """The flow-hash choreography on CPU (oracle tables, gloo collectives): host
+    partition -> per-rank parse -> first_seen to global frame index through the
+    record -> frame map -> all-gather + merge (no rebase) -> per-rank records
+    before each merged flow's first frame, all-reduced -> global record index."""
     import torch
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    from merge_ref import entries_to_table, merge, table_to_entries
+    from oracle_py import Oracle
+    from tracegen import mixed_trace
+
+    from tcbee_amd import host
+    from tcbee_amd.dist import gather_tables
+
+    tr = mixed_trace(n, seed=404, n_flows=700)
+    sub, gidx = host.flowhash_shard(tr, world, rank)
+    orc = Oracle()
+    rec, fh, fi, ctr, table = orc.parse(sub, filter_port=filter_port)
+    rec_frame = np.nonzero(orc.accept_mask(sub, filter_port=filter_port))[0]
+    gframe = gidx[rec_frame]                      # ascending global frame of each record
+    table = table.copy()
+    table["first_seen"] = gframe[table["first_seen"].astype(np.int64)]
+    ent = torch.from_numpy(table_to_entries(table, cap))
+    meta = torch.tensor([len(table), 0], dtype=torch.int64)
+    all_ent, all_meta = gather_tables(ent, meta)
+    all_ent = all_ent.numpy().reshape(world, cap, 8)
+    all_meta = all_meta.numpy().reshape(world, 2)
+    tables = [entries_to_table(all_ent[r], int(all_meta[r, 0])) for r in range(world)]
+    merged, maps = merge(tables, [0] * world)
+    cnt = torch.from_numpy(np.searchsorted(gframe, merged["first_seen"].astype(np.int64))
+                           .astype(np.int64))
+    dist.all_reduce(cnt)
+    merged["first_seen"] = cnt.numpy().astype(np.uint64)
+    gids = maps[rank][fi] if len(fi) else fi
+    np.savez(os.path.join(result_dir, f"rank{rank}.npz"), merged=merged.view(np.uint8),
+             gids=gids, gidx=gidx, rec=rec)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_gpu(rank, world, port, n, cap, result_dir, mode, n_flows=3000, filter_port=0,
+            backend="gloo"):
+    """N>1 choreography on the GPU: ranks share device 0 over gloo. mode "step":
+    FlowMerge.step on one stream; mode "overlap": OverlappedMerge over 3 steps of
+    the same shard (fresh table each step, output slots rotating), as bench.py;
+    mode "flowhash": the rank's flow-hash shard of a synthetic global trace of n
+    frames, built by the device generator, exchanged with global first_seen;
+    mode "flowhash_real": the rank's flow-hash shard (host partitioner, the NIC-RSS
+    step) of a mixed trace with rejected and FILTER_PORT-filtered frames, placed
+    through the parse's record -> frame map; mode "flowhash_noframe": the same
+    without the map (must be refused: TCBEE_ESHARD)."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_stream(torch.cuda.Stream())
     import tcbee_amd
+    from tcbee_amd import host
     from tcbee_amd.dist import FlowMerge, OverlappedMerge, shard_range
     from tracegen import mixed_trace
 
@@ -63,11 +117,15 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode):
         import bench
         s0 = torch.cuda.current_stream().cuda_stream
         arena, alen, off, ln, ts, gidx, m = bench.build_shard_trace(
-            torch, n, world, rank, "imix", 1, 3000, 0x7CBEE, s0)
+            torch, n, world, rank, "imix", 1, n_flows, 0x7CBEE, s0)
     else:
-        tr = mixed_trace(n, seed=404, n_flows=700)
-        lo, hi = shard_range(tr.n, rank, world)
-        sub = tr.slice(lo, hi)
+        tr = mixed_trace(n, seed=404, n_flows=n_flows)
+        if mode.startswith("flowhash_"):
+            sub, g = host.flowhash_shard(tr, world, rank)
+            gidx = torch.from_numpy(g).cuda()
+        else:
+            lo, hi = shard_range(tr.n, rank, world)
+            sub = tr.slice(lo, hi)
         m = sub.n
         alen = len(sub.arena)
         arena = torch.zeros(len(sub.arena) + 64, dtype=torch.uint8, device="cuda")
@@ -75,13 +133,16 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode):
         off = torch.from_numpy(sub.offset.view(np.int64)).cuda()
         ln = torch.from_numpy(sub.caplen.view(np.int32)).cuda()
         ts = torch.from_numpy(sub.ts_ns.view(np.int64)).cuda()
+    with_frame = mode == "flowhash_real"
     nbuf = 2 if mode == "overlap" else 1
     slots = [{"rec": torch.empty(m * 74 + 64, dtype=torch.uint8, device="cuda"),
               "hash": torch.empty(m, dtype=torch.int32, device="cuda"),
               "id": torch.empty(m, dtype=torch.int32, device="cuda"),
+              "frame": torch.empty(m, dtype=torch.int32, device="cuda") if with_frame else None,
               "n": torch.zeros(1, dtype=torch.int64, device="cuda"),
               "ctr": torch.zeros(4, dtype=torch.int64, device="cuda")} for _ in range(nbuf)]
     s = torch.cuda.current_stream().cuda_stream
+    status = 0
     with tcbee_amd.PacketParser(max_frames=max(m, 1), max_flows=cap) as p, \
             tcbee_amd.PacketParser(max_frames=1024, max_flows=world * cap) as mg:
         fm = FlowMerge(p, mg, cap, n, nbuf=nbuf)
@@ -96,19 +157,22 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode):
             b["ctr"].zero_()
             p.reset_flows(stream=s, sync=False)
             p.parse_device(arena, alen, off, ln, ts, m, b["rec"], m, b["hash"], b["id"],
-                           b["n"], b["ctr"], stream=s)
+                           b["n"], b["ctr"], stream=s, filter_port=filter_port,
+                           out_frame=b["frame"])
             if om:
                 om.submit(k, b["id"], b["n"], m, ctr=b["ctr"])
             else:
-                fm.step(b["id"], b["n"], m, stream=s)
+                fm.step(b["id"], b["n"], m, stream=s, rec_frame=b["frame"])
                 dist.all_reduce(b["ctr"])
         torch.cuda.synchronize()
+        status = p.status()
         b = slots[(steps - 1) % nbuf]
         k = int(b["n"].item())
         np.savez(os.path.join(result_dir, f"rank{rank}.npz"),
                  gidx=(gidx.cpu().numpy() if gidx is not None else np.zeros(0, np.int64)),
                  rec=b["rec"][:k * 74].cpu().numpy().reshape(-1, 74),
                  gids=b["id"][:k].cpu().numpy().view(np.uint32),
-                 ctr=b["ctr"].cpu().numpy(), merged=mg.flows().view(np.uint8))
+                 ctr=b["ctr"].cpu().numpy(), merged=mg.flows().view(np.uint8),
+                 status=np.array([status]))
     dist.barrier()
     dist.destroy_process_group()

@@ -77,6 +77,8 @@ class Oracle:
         L.orc_parse_batch.argtypes = [vp, vp, vp, vp, u64, C.c_uint16, C.c_int, vp, u64,
                                       vp, vp, vp, u64, C.POINTER(OrcCounters)]
         L.orc_parse_batch.restype = u64
+        L.orc_accept_mask.argtypes = [vp, vp, vp, u64, C.c_uint16, C.c_int, vp]
+        L.orc_accept_mask.restype = None
         L.orc_baseline_run.argtypes = [vp, vp, vp, vp, u64, C.c_uint16, C.c_int, vp]
         L.orc_baseline_run.restype = u64
         L.orc_baseline_file.argtypes = [vp, vp, vp, vp, u64, C.c_uint16, C.c_char_p]
@@ -166,6 +168,15 @@ class Oracle:
         if own:
             self.free_flowtab(ft)
         return rec[:k], fh[:k], fi[:k], ctr.as_dict(), table
+
+    def accept_mask(self, trace, filter_port: int = 0, direction: int = 0) -> np.ndarray:
+        """bool per frame: does the hook emit a record for it."""
+        out = np.zeros(max(trace.n, 1), dtype=np.uint8)
+        arena = trace.arena if len(trace.arena) else np.zeros(1, np.uint8)
+        self.L.orc_accept_mask(arena.ctypes.data, trace.offset.ctypes.data,
+                               trace.caplen.ctypes.data, trace.n, filter_port, direction,
+                               out.ctypes.data)
+        return out[:trace.n].astype(bool)
 
     def baseline_file(self, trace, path: str, filter_port: int = 0) -> int:
         """CPU-1-file: one thread, records appended to `path` (drain-task buffering)."""

@@ -30,9 +30,10 @@ def test_library_loads_and_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     L = tcbee_amd.lib()
-    assert L.tcbee_abi_version() == 1
+    assert L.tcbee_abi_version() == 2
     assert L.tcbee_strerror(0) == b"ok"
     assert L.tcbee_strerror(_lib.EFLOWFULL) == b"flow table full"
+    assert b"first record" in L.tcbee_strerror(_lib.ESHARD)
 
 
 def test_device_count_does_not_crash():
@@ -45,6 +46,14 @@ def test_ctx_create_fails_loudly_without_gpu():
     with pytest.raises(tcbee_amd.TcbeeError) as e:
         tcbee_amd.PacketParser(max_frames=16)
     assert e.value.code == _lib.ENODEV
+
+
+def test_ctx_create_rejects_oversized_table():
+    """max_flows past 2^24 (a 2 GiB table: K1's probe buffer resource and u32 slot
+    offsets end there) is refused before any device work (VERDICT r1 weak #8)."""
+    with pytest.raises(tcbee_amd.TcbeeError) as e:
+        tcbee_amd.PacketParser(max_frames=16, max_flows=(1 << 24) + 1)
+    assert e.value.code == _lib.ECAPACITY
 
 
 def test_flow_hash_matches_oracle(oracle):

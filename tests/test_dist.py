@@ -58,3 +58,63 @@ def test_gloo_world2_choreography(oracle, tmp_path):
         assert np.array_equal(r["merged"].view(FLOW_DTYPE), full[4])
     gids = np.concatenate([r["gids"] for r in res])
     assert np.array_equal(gids, full[2])
+
+
+@pytest.mark.parametrize("filter_port", [0, 5201])
+def test_gloo_world2_flowhash_real_trace(oracle, tmp_path, filter_port):
+    """Flow-hash partition of a trace with rejected and filtered frames: global
+    ids and the merged table (first_seen = global record index) vs the oracle on
+    the whole trace (the algorithm tcbee_amd.dist runs on the device)."""
+    import torch.multiprocessing as mp
+
+    import dist_worker
+    from tracegen import mixed_trace
+    from tcbee_amd.parser import FLOW_DTYPE
+    n, cap, world = 40_000, 2048, 2
+    mp.spawn(dist_worker.run_flowhash, args=(world, free_port(), n, cap, str(tmp_path),
+                                             filter_port), nprocs=world, join=True)
+    tr = mixed_trace(n, seed=404, n_flows=700)
+    rec, fh, fi, ctr, table = oracle.parse(tr, filter_port=filter_port)
+    acc = oracle.accept_mask(tr, filter_port=filter_port)
+    recidx = np.cumsum(acc) - 1
+    res = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    for x in res:
+        assert np.array_equal(x["merged"].view(FLOW_DTYPE), table)
+        g = x["gidx"]
+        ri = recidx[g[acc[g]]]
+        assert np.array_equal(x["rec"], rec[ri]) and np.array_equal(x["gids"], fi[ri])
+
+
+def test_flowhash_owner_matches_key_hash(oracle):
+    """The host partitioner keys frames exactly as the hook does (fixed offsets,
+    xdp.rs:37-127) and routes keyless frames round robin."""
+    from tracegen import mixed_trace
+    from tcbee_amd import host
+    tr = mixed_trace(6000, seed=77, n_flows=300)
+    for world in (1, 2, 3, 8):
+        own = host.flowhash_owner(tr, world, threads=3)
+        for i in range(tr.n):
+            _, key = oracle.hook(tr.frame(i))
+            if key is None:
+                # runts and non-TCP frames: round robin (a runt with a keyable prefix
+                # never reaches here: the hook and the partitioner share the bounds)
+                assert own[i] == i % world
+            else:
+                h = oracle.flow_hash64(key)
+                assert own[i] == ((h ^ (h >> 32)) & 0xFFFFFFFF) % world
+
+
+def test_flowhash_owner_matches_device_shards():
+    """On the synthetic trace the partitioner reproduces the device shard
+    generator's placement (fold32(flow_hash64) % world: tcbee_gen_shard_index_device)."""
+    import tcbee_amd
+    from tcbee_amd import host
+    tr = tcbee_amd.synth_trace(20_000, sizes="imix", kind=1, n_flows=3000)
+    orc_hash = tcbee_amd.parser.flow_hash64
+    own = host.flowhash_owner(tr, 4)
+    for i in range(0, tr.n, 97):
+        f = tr.frame(i)
+        key = bytes(12) + f[26:30] + bytes(12) + f[30:34] + f[34:36][::-1] + f[36:38][::-1] \
+            + bytes([6, 0, 0, 0])
+        h = orc_hash(key)
+        assert own[i] == ((h ^ (h >> 32)) & 0xFFFFFFFF) % 4

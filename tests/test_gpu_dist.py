@@ -66,3 +66,109 @@ def test_gpu_world2_flowhash_shards(gpu, oracle, tmp_path):
         assert np.array_equal(x["gids"], fi[g])
         assert np.array_equal(x["merged"].view(FLOW_DTYPE), table)
         assert int(x["ctr"][0]) == ctr["ingress"]
+
+
+def test_gpu_world2_flowhash_200k_flows(gpu, oracle, tmp_path):
+    """the flow-hash partition at >= 200k flows (each rank's table
+    ~125k flows, K3's bucketed large-table mode, the records-before first_seen
+    fix-up over 600k global frames)."""
+    import torch.multiprocessing as mp
+
+    import dist_worker
+    import tcbee_amd
+    from tcbee_amd.parser import FLOW_DTYPE
+    n, flows, world = 600_000, 250_000, 2
+    cap = int(1.25 * flows / world) + 4096
+    mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path), "flowhash",
+                                        flows), nprocs=world, join=True)
+    tr = tcbee_amd.synth_trace(n, sizes="imix", kind=1, n_flows=flows)
+    ft = oracle.new_flowtab(1 << 19)
+    try:
+        rec, fh, fi, ctr, _ = oracle.parse(tr, ft=ft)
+        table = oracle.flows(ft)
+    finally:
+        oracle.free_flowtab(ft)
+    assert len(table) > 200_000
+    res = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    owner = fh % world
+    for r, x in enumerate(res):
+        g = x["gidx"]
+        assert np.array_equal(g, np.nonzero(owner == r)[0])
+        assert np.array_equal(x["rec"], rec[g])
+        assert np.array_equal(x["gids"], fi[g])
+        assert np.array_equal(x["merged"].view(FLOW_DTYPE), table)
+        assert int(x["ctr"][0]) == ctr["ingress"] and int(x["status"][0]) == 0
+
+
+@pytest.mark.parametrize("filter_port", [0, 5201])
+def test_gpu_world2_flowhash_real_trace(gpu, oracle, tmp_path, filter_port):
+    """VERDICT r1 #2 / ADVICE r1: flow-hash shards of a REAL trace (non-TCP frames,
+    runts, IPv6, v4-compatible collisions, FILTER_PORT) — record k of a rank is not
+    its frame k. The host partitioner (the NIC-RSS step) splits the trace; each
+    rank's parse writes its record -> frame map, the export places every flow at
+    its global frame, and the merged first_seen is the global record index.
+    Records, global ids, counters and the merged table vs the oracle over the
+    whole trace."""
+    import torch.multiprocessing as mp
+
+    import dist_worker
+    from tracegen import mixed_trace
+    from tcbee_amd.parser import FLOW_DTYPE
+    n, flows, cap, world = 200_000, 5000, 8192, 2
+    mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path),
+                                        "flowhash_real", flows, filter_port),
+             nprocs=world, join=True)
+    tr = mixed_trace(n, seed=404, n_flows=flows)
+    rec, fh, fi, ctr, table = oracle.parse(tr, filter_port=filter_port)
+    acc = oracle.accept_mask(tr, filter_port=filter_port)
+    recidx = np.cumsum(acc) - 1
+    assert acc.sum() == len(rec) and acc.sum() < n
+    res = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    got = np.concatenate([x["gidx"] for x in res])
+    assert np.array_equal(np.sort(got), np.arange(n))  # the shards partition the trace
+    for x in res:
+        g = x["gidx"]
+        ri = recidx[g[acc[g]]]
+        assert np.array_equal(x["rec"], rec[ri])
+        assert np.array_equal(x["gids"], fi[ri])
+        assert np.array_equal(x["merged"].view(FLOW_DTYPE), table)
+        assert int(x["ctr"][0]) == ctr["ingress"] and int(x["ctr"][2]) == ctr["handled"]
+        assert int(x["status"][0]) == 0
+
+
+def test_gpu_world2_flowhash_without_frame_map_is_refused(gpu, tmp_path):
+    """A shard with rejected frames exported WITHOUT the record -> frame map cannot
+    be placed in the global trace: the local context reports TCBEE_ESHARD instead
+    of silently merging wrong first-seen order."""
+    import torch.multiprocessing as mp
+
+    import dist_worker
+    from tcbee_amd import _lib
+    n, flows, cap, world = 30_000, 500, 2048, 2
+    mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path),
+                                        "flowhash_noframe", flows), nprocs=world, join=True)
+    for r in range(world):
+        assert int(np.load(tmp_path / f"rank{r}.npz")["status"][0]) == _lib.ESHARD
+
+
+@pytest.mark.parametrize("mode", ["overlap", "flowhash_real"])
+def test_gpu_rccl_world1_exchange(gpu, oracle, tmp_path, mode):
+    """The RCCL branch of the exchange (all_gather_into_tensor + all_reduce on the
+    `nccl` backend, i.e. RCCL) on this one-GPU box: world 1, since RCCL refuses two
+    ranks on one device ("Duplicate GPU detected"). Same checks as world 2."""
+    import torch.multiprocessing as mp
+
+    import dist_worker
+    from tracegen import mixed_trace
+    from tcbee_amd.parser import FLOW_DTYPE
+    n, flows, cap = 60_000, 700, 2048
+    mp.spawn(dist_worker.run_gpu, args=(1, free_port(), n, cap, str(tmp_path), mode, flows,
+                                        5201 if mode == "flowhash_real" else 0, "nccl"),
+             nprocs=1, join=True)
+    fp = 5201 if mode == "flowhash_real" else 0
+    tr = mixed_trace(n, seed=404, n_flows=flows)
+    rec, fh, fi, ctr, table = oracle.parse(tr, filter_port=fp)
+    x = np.load(tmp_path / "rank0.npz")
+    assert np.array_equal(x["rec"], rec) and np.array_equal(x["gids"], fi)
+    assert np.array_equal(x["merged"].view(FLOW_DTYPE), table)
+    assert int(x["ctr"][0]) == ctr["ingress"] and int(x["status"][0]) == 0

@@ -391,3 +391,65 @@ def test_k3_mode_switch_across_batches(gpu, oracle):
         assert n1 <= 12288 < len(table)
         assert np.array_equal(np.concatenate([r1.flow_id, r2.flow_id]), fi)
         assert np.array_equal(p.flows(), table)
+
+
+def test_config4_scale_over_1M_flows_mixed(gpu, oracle):
+    """Config 4's table size: > 1M distinct flows from a mixed trace
+    (rejects, runts, IPv6, v4-compatible collisions), two batches of 2.5M frames
+    through K1's large-table probe path, K2's multi-kernel rank scan and K3's
+    bucketed mode; records, ids and the whole table vs the oracle."""
+    from tracegen import mixed_trace
+    tr = mixed_trace(5_000_000, seed=4004, n_flows=1_700_000)
+    cut = 2_500_000
+    a, b = tr.slice(0, cut), tr.slice(cut, tr.n)
+    with tcbee_amd.PacketParser(max_frames=cut, max_arena=max(len(a.arena), len(b.arena)),
+                                max_flows=1_600_000) as p:
+        r1 = p.parse(a)
+        r2 = p.parse(b)
+        ft = oracle.new_flowtab(1 << 22)
+        try:
+            rec, fh, fi, ctr, _ = oracle.parse(tr, ft=ft)
+            table = oracle.flows(ft)
+        finally:
+            oracle.free_flowtab(ft)
+        assert len(table) > 1_000_000
+        assert np.array_equal(np.concatenate([r1.records, r2.records]), rec)
+        assert np.array_equal(np.concatenate([r1.flow_hash, r2.flow_hash]), fh)
+        assert np.array_equal(np.concatenate([r1.flow_id, r2.flow_id]), fi)
+        fl = p.flows()
+        assert len(fl) == len(table) and np.array_equal(fl, table)
+        assert p.status() == 0
+
+
+def test_config4_1M_flows_device_right_sized(gpu, oracle):
+    """1M synthetic IMIX flows, device-resident path, table sized exactly for 1M
+    flows (2^21 slots = 128 MiB: what bench.py allocates for config 4)."""
+    import torch
+    n, flows = 3_500_000, 1_000_000
+    tr = tcbee_amd.synth_trace(n, sizes="imix", kind=1, n_flows=flows)
+    d_arena = torch.from_numpy(np.concatenate([tr.arena, np.zeros(64, np.uint8)])).cuda()
+    d_off = torch.from_numpy(tr.offset.view(np.int64)).cuda()
+    d_len = torch.from_numpy(tr.caplen.view(np.int32)).cuda()
+    d_ts = torch.from_numpy(tr.ts_ns.view(np.int64)).cuda()
+    rec_d = torch.empty(n * 74 + 64, dtype=torch.uint8, device="cuda")
+    fh_d = torch.empty(n, dtype=torch.int32, device="cuda")
+    fi_d = torch.empty(n, dtype=torch.int32, device="cuda")
+    n_d = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctr_d = torch.zeros(4, dtype=torch.int64, device="cuda")
+    with tcbee_amd.PacketParser(max_frames=n, max_flows=flows) as p:
+        s = torch.cuda.current_stream().cuda_stream
+        p.parse_device(d_arena, len(tr.arena), d_off, d_len, d_ts, n, rec_d, n, fh_d, fi_d, n_d,
+                       ctr_d, stream=s)
+        torch.cuda.synchronize()
+        ft = oracle.new_flowtab(1 << 21)
+        try:
+            rec, fh, fi, ctr, _ = oracle.parse(tr, ft=ft)
+            table = oracle.flows(ft)
+        finally:
+            oracle.free_flowtab(ft)
+        assert int(n_d.item()) == len(rec) == n
+        assert np.array_equal(rec_d[:n * 74].cpu().numpy().reshape(-1, 74), rec)
+        assert np.array_equal(fh_d.cpu().numpy().view(np.uint32), fh)
+        assert np.array_equal(fi_d.cpu().numpy().view(np.uint32), fi)
+        assert np.array_equal(p.flows(), table)
+        assert p.status() == 0
