@@ -121,12 +121,12 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     # flow-hash shards hold ~n_flows/world flows each; the exchange carries `xcap`
     # entries per rank (checked against the real count after the run)
     flows_here = -(-n_flows // sw) if flowhash else n_flows
-    # table sized for the flows the trace can hold (>= 2x slots, power of two): a
-    # contiguous shard sees at most n_flows, a flow-hash shard n_flows / N plus a
-    # few standard deviations of the hash split (the table accepts more anyway, up
-    # to its slot count; `status` would report a full one)
-    cap = flows_here + (8 * int(flows_here ** 0.5) + 64 if flowhash and sw > 1 else 0)
-    cap = max(cap, 1 << 12)
+    # table: max_flows = 4x the shard's flows (>= 8 slots per flow, load <= 1/8).
+    # Linear-probe collisions cost K1 a random 64-B line each, and they grow with
+    # the load: at load 1/2 (max_flows = flows, 128 MiB for 1M flows) K1 is 6 %
+    # slower at 10k flows, 31 % at 125k and 36 % at 1M; 8x/16x gain < 3 % on K1 and
+    # lose it to the bigger per-step table reset (profiles/r02_capsweep.json)
+    cap = max(4 * flows_here, 1 << 12)
     # (the exchange carries up to xcap entries per rank: a quarter more than the
     # shard's expected flows)
     xcap = max(int(1.25 * flows_here) + 4096, 1 << 12)
@@ -343,11 +343,28 @@ def cpu_baseline(sizes, kind, n_flows, seed, seconds, threads, sample_n=2_000_00
 
 
 def host_cores() -> int:
-    """CPUs this process may run on (what `nproc` prints)."""
+    """The host cores this job may use: what `nproc` prints (coreutils honours
+    OMP_NUM_THREADS, which the GPU box sets to the job's CPU share, 16 per GPU;
+    os.cpu_count() there is the whole machine's 256 logical CPUs, and 256
+    threads on a 16-CPU share oversubscribe it)."""
+    import subprocess
     try:
-        return len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        return os.cpu_count() or 1
+        return max(1, int(subprocess.run(["nproc"], capture_output=True, text=True,
+                                         timeout=10).stdout.strip()))
+    except (OSError, ValueError, subprocess.SubprocessError):
+        try:
+            return len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            return os.cpu_count() or 1
+
+
+def cgroup_cpus():
+    """CPU quota of this cgroup (cpu.max), None if unlimited/unknown."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=5, threads=None):
@@ -599,7 +616,7 @@ def main():
             v, done, el = res[threads]
             out["cpu_baseline"] = {
                 "value": round(v, 2), "unit": "Mpkt/s", "cores": threads, "kind": "port",
-                "nproc": threads, "machine_cpus": os.cpu_count(),
+                "nproc": threads, "machine_cpus": os.cpu_count(), "cgroup_cpus": cgroup_cpus(),
                 "sample": (f"{sample_n} frames of the same workload, repeated {done // sample_n}x "
                            f"({el:.1f}s); oracle/tcbee_oracle.c orc_baseline_run = xdp_hook + "
                            "per-thread FLOWS(100) + bincode serialize"),

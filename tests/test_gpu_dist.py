@@ -28,7 +28,7 @@ def test_gpu_world2_merge(gpu, oracle, tmp_path, mode):
     from tracegen import mixed_trace
     from tcbee_amd.parser import FLOW_DTYPE
     n, cap, world = 60_000, 2048, 2
-    mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path), mode),
+    mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path), mode, 700),
              nprocs=world, join=True)
     tr = mixed_trace(n, seed=404, n_flows=700)
     rec, fh, fi, ctr, table = oracle.parse(tr)

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--workloads", default="imix10k,imix1,64B1")
     ap.add_argument("--var", default="", help="extra env A/B, e.g. TCBEE_K3ABL=0,2")
     ap.add_argument("--flows-only", action="store_true", help="only the flows-on variants")
-    ap.add_argument("--cap-mult", type=float, default=4.0, help="max_flows = mult x flows")
+    ap.add_argument("--cap-mult", default="4", help="max_flows = mult x flows (comma list: A/B)")
     args = ap.parse_args()
     import torch
     import tcbee_amd
@@ -54,14 +54,15 @@ def main():
         var_name, _, var_vals = args.var.partition("=")
         vvals = var_vals.split(",") if var_name else [""]
         variants = list(itertools.product(args.fpl.split(","),
-                                          [True] if args.flows_only else [True, False], vvals))
+                                          [True] if args.flows_only else [True, False], vvals,
+                                          [float(x) for x in args.cap_mult.split(",")]))
         parsers = {}
-        for fpl, flows, vv in variants:
+        for fpl, flows, vv, cm in variants:
             os.environ["TCBEE_FPL"] = fpl
             if var_name:
                 os.environ[var_name] = vv
-            parsers[(fpl, flows, vv)] = tcbee_amd.PacketParser(max_frames=n,
-                                                               max_flows=max(int(args.cap_mult * nf), 4096))
+            parsers[(fpl, flows, vv, cm)] = tcbee_amd.PacketParser(
+                max_frames=n, max_flows=max(int(cm * nf), 4096))
         times = {v: [] for v in variants}
         k1 = {v: [] for v in variants}
         for r in range(args.rounds):
@@ -85,7 +86,8 @@ def main():
                 times[v].append(el * 1e3)
                 k1[v].append(ms / max(k, 1))
         for v in variants:
-            key = f"{wl} fpl={v[0]} flows={int(v[1])}" + (f" {var_name}={v[2]}" if var_name else "")
+            key = (f"{wl} fpl={v[0]} flows={int(v[1])}" + (f" {var_name}={v[2]}" if var_name else "")
+                   + (f" cap={v[3]:g}x" if "," in args.cap_mult else ""))
             step_ms = float(np.median(times[v]))
             k1_ms = float(np.median(k1[v]))
             results[key] = {"step_ms": round(step_ms, 4), "k1_ms": round(k1_ms, 4),
