@@ -17,7 +17,9 @@ from ._lib import EDB, EFORMAT, OK, Counters, Frames, RECORD_BYTES, TcbeeError
 from .trace import Trace
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-HOST_LIB_PATH = os.path.join(_HERE, "lib", "libtcbee_host.so")
+# TCBEE_HOST_LIB: an alternative build of the same library (the sanitizer build
+# tests/test_sanitize.py loads)
+HOST_LIB_PATH = os.environ.get("TCBEE_HOST_LIB") or os.path.join(_HERE, "lib", "libtcbee_host.so")
 
 SINK_DURABLE = 0x1
 # DataValue::type_to_int (ts-storage/src/lib.rs:74-95)

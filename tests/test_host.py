@@ -385,3 +385,28 @@ def test_oracle_replays_fixture_too(tmp_path):
     db.insert_multiple_points(ts1, 0, [(99.0, 3), (100.0, 4)])
     db.close()
     assert process_ref.dump_db(path) == {k: [list(r) for r in v] for k, v in fx["rows"].items()}
+
+
+def test_config1_loopback_trace_through_sink(oracle, tmp_path):
+    """Config 1's shape on the CPU side: the loopback iperf3 capture's oracle records
+    (both hooks; flags always 0 despite SYN/FIN) through the tcbee-process stage
+    (xdp.tcp then tc.tcp) equal process_ref's database: two flows, no flag series."""
+    import numpy as np
+
+    from tracegen import iperf3_loopback_trace
+    from tcbee_amd.trace import Trace
+    t = iperf3_loopback_trace(4000)
+    t2 = Trace(t.arena, t.offset, t.caplen, t.ts_ns - np.uint64(1500))
+    rx, rt = oracle.parse(t), oracle.parse(t2, direction=1)
+    assert len(rx[0]) == len(rt[0]) == t.n and len(rx[4]) == 2
+    assert not rx[0][:, 62:68].any()
+    prefix = str(tmp_path) + "/lo_"
+    open(prefix + "xdp.tcp", "wb").write(rx[0].tobytes())
+    open(prefix + "tc.tcp", "wb").write(rt[0].tobytes())
+    host.process_files(prefix, str(tmp_path / "g.sqlite"))
+    process_ref.process_records(rx[0].tobytes() + rt[0].tobytes(), str(tmp_path / "o.sqlite"))
+    got = process_ref.dump_db(str(tmp_path / "g.sqlite"))
+    assert got == process_ref.dump_db(str(tmp_path / "o.sqlite"))
+    assert [r[1:] for r in got["flows"]][0][3:] == [5201, 6]
+    names = {r[2] for r in got["time_series"]}
+    assert not any(n.startswith("FLAG_") for n in names)

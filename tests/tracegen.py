@@ -102,3 +102,74 @@ def mixed_trace(n: int, seed: int = 1, n_flows: int = 64, max_gap: int = 3,
 
     ts = np.uint64(TS_BASE_NS) + np.uint64(TS_STEP_NS) * np.arange(n, dtype=np.uint64)
     return Trace(arena[:total], off.astype(np.uint64), ln.astype(np.uint32), ts)
+
+
+def iperf3_loopback_trace(n: int = 10_000, seed: int = 5201, snaplen: int = 96,
+                          ts0: int = 5_000_000_000_000, gap_ns: int = 800) -> Trace:
+    """A loopback iperf3 TCP transfer as `tcpdump -i lo -s <snaplen>` would capture
+    it (config 1 of BASELINE.json: tcbee-record/run.sh:2 records `lo` while iperf3
+    runs): all-zero MACs, 127.0.0.1 both ends, ONE connection (two IpTuples,
+    client->server data and server->client ACKs): SYN / SYN-ACK / ACK with
+    option-bearing headers (doff 10 / 8), PSH-ACK data segments of lo's 65483-B
+    MSS (captured to `snaplen`), an ACK every second segment, FIN-ACK / FIN-ACK /
+    ACK at the end. Timestamps are ktime-like (ns since boot)."""
+    rng = np.random.default_rng(seed)
+    cport, sport = 40_000 + int(rng.integers(0, 20_000)), 5201
+    isn_c, isn_s = (int(x) for x in rng.integers(0, 2**32, size=2))
+    mss = 65483 - 12
+    frames = []  # (dir 0 = client->server, flags, seq, ack, tcp_hdr_len, payload)
+    frames.append((0, 0x02, isn_c, 0, 40, 0))
+    frames.append((1, 0x12, isn_s, (isn_c + 1) % 2**32, 40, 0))
+    frames.append((0, 0x10, isn_c + 1, isn_s + 1, 32, 0))
+    seq_c, seq_s = isn_c + 1, isn_s + 1
+    k = 0
+    while len(frames) < n - 3:
+        frames.append((0, 0x18, seq_c % 2**32, seq_s % 2**32, 32, mss))
+        seq_c += mss
+        k += 1
+        if k % 2 == 0 and len(frames) < n - 3:
+            frames.append((1, 0x10, seq_s % 2**32, seq_c % 2**32, 32, 0))
+    frames.append((0, 0x11, seq_c % 2**32, seq_s % 2**32, 32, 0))
+    frames.append((1, 0x11, seq_s % 2**32, (seq_c + 1) % 2**32, 32, 0))
+    frames.append((0, 0x10, (seq_c + 1) % 2**32, (seq_s + 1) % 2**32, 32, 0))
+    out = []
+    ip_id = [int(rng.integers(0, 65536)), int(rng.integers(0, 65536))]
+    for d, flags, seq, ack, th, pay in frames:
+        flen = 14 + 20 + th + pay
+        tot = 20 + th + pay
+        b = bytearray(min(flen, snaplen))
+        hdr = bytearray(14 + 20 + th)
+        hdr[12:14] = b"\x08\x00"                       # MACs stay zero on lo
+        ip = bytearray(20)
+        ip[0], ip[1] = 0x45, 0
+        ip[2:4] = tot.to_bytes(2, "big") if tot < 65536 else b"\xff\xff"
+        ip[4:6] = (ip_id[d] & 0xFFFF).to_bytes(2, "big")
+        ip_id[d] += 1
+        ip[6:8] = b"\x40\x00"                          # DF
+        ip[8], ip[9] = 64, 6
+        ip[12:16] = bytes([127, 0, 0, 1])
+        ip[16:20] = bytes([127, 0, 0, 1])
+        s = sum(int.from_bytes(ip[j:j + 2], "big") for j in range(0, 20, 2))
+        s = (s & 0xFFFF) + (s >> 16)
+        s = (s & 0xFFFF) + (s >> 16)
+        ip[10:12] = (~s & 0xFFFF).to_bytes(2, "big")
+        hdr[14:34] = ip
+        t = bytearray(th)
+        t[0:2] = (cport if d == 0 else sport).to_bytes(2, "big")
+        t[2:4] = (sport if d == 0 else cport).to_bytes(2, "big")
+        t[4:8] = seq.to_bytes(4, "big")
+        t[8:12] = ack.to_bytes(4, "big")
+        t[12] = (th // 4) << 4
+        t[13] = flags
+        t[14:16] = (65495 if flags & 0x02 else 512).to_bytes(2, "big")
+        t[16:18] = int(rng.integers(0, 65536)).to_bytes(2, "big")  # lo: partial checksum
+        if th > 20:
+            t[20:22] = b"\x01\x01"                     # NOP NOP
+            t[22:24] = b"\x08\x0a"                     # timestamps option
+            t[24:28] = int(rng.integers(0, 2**32)).to_bytes(4, "big")
+        hdr[34:34 + th] = t
+        m = min(len(hdr), len(b))
+        b[:m] = hdr[:m]
+        out.append(bytes(b))
+    ts = np.uint64(ts0) + np.uint64(gap_ns) * np.arange(len(out), dtype=np.uint64)
+    return Trace.from_frames(out, ts_ns=ts)
