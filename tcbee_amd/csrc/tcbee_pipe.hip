@@ -27,7 +27,12 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
-#include <immintrin.h>
+#if defined(__x86_64__)
+#include <immintrin.h>  // streaming stores of the header-window gather (x86 hosts)
+#define TCBEE_PIPE_HAVE_NT 1
+#else
+#define TCBEE_PIPE_HAVE_NT 0
+#endif
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -235,7 +240,9 @@ void stage(tcbee_pipe* p, const tcbee_frames* in, Slot& s) {
   if (W) {
     const uint64_t pf = p->prefetch;
     // (16-B streaming stores need a 16-B aligned staging slot per frame)
-    const bool nt = p->nt_copy && W % 16 == 0 && ((uintptr_t)s.h_arena & 15u) == 0;
+    // (streaming stores exist on x86 hosts only; elsewhere the memcpy path runs)
+    const bool nt = TCBEE_PIPE_HAVE_NT && p->nt_copy && W % 16 == 0 &&
+                    ((uintptr_t)s.h_arena & 15u) == 0;
     p->pool->run([&](unsigned part, unsigned parts) {
       const uint64_t a = n * part / parts, b = n * (part + 1) / parts;
       for (uint64_t k = a; k < b; ++k) {
@@ -251,6 +258,7 @@ void stage(tcbee_pipe* p, const tcbee_frames* in, Slot& s) {
         }
         const uint32_t len = in->caplen[f];
         const uint64_t o = in->offset[f];
+#if TCBEE_PIPE_HAVE_NT
         if (nt && o + W <= in->arena_len) {
           // the whole window, whatever the caplen: the bytes past caplen are never
           // read (the kernels take caplen from h_len), so no per-frame length
@@ -262,6 +270,7 @@ void stage(tcbee_pipe* p, const tcbee_frames* in, Slot& s) {
           s.h_ts[k] = in->ts_ns[f];
           continue;
         }
+#endif
         const uint64_t want = len < W ? len : W;
         uint64_t cp = want;
         if (o >= in->arena_len) cp = 0;
@@ -271,7 +280,9 @@ void stage(tcbee_pipe* p, const tcbee_frames* in, Slot& s) {
         s.h_len[k] = len;
         s.h_ts[k] = in->ts_ns[f];
       }
+#if TCBEE_PIPE_HAVE_NT
       if (nt) _mm_sfence();  // streaming stores visible before the H2D copy is issued
+#endif
     });
     s.arena_used = n * W;
     return;

@@ -32,10 +32,15 @@ def check_same(res, orc, flows_gpu=None):
         assert np.array_equal(flows_gpu, table)
 
 
+@pytest.mark.parametrize("nt", ["1", "0"])
 @pytest.mark.parametrize("window,chunk,depth,threads", [
     (80, 4096, 3, 8), (80, 1000, 4, 1), (0, 4096, 3, 8), (96, 65536, 5, 3), (0, 777, 3, 2),
 ])
-def test_pipeline_matches_oracle(gpu, oracle, window, chunk, depth, threads):
+def test_pipeline_matches_oracle(gpu, oracle, window, chunk, depth, threads, nt, monkeypatch):
+    """TCBEE_PIPE_NT=1 (default): the header-window gather copies whole windows with
+    streaming stores, so the staged bytes past a frame's caplen are the NEXT frame's
+    (mixed_trace's arena is random bytes everywhere); =0: memcpy of caplen bytes."""
+    monkeypatch.setenv("TCBEE_PIPE_NT", nt)
     t = mixed_trace(60_000, seed=100 + chunk, n_flows=300)
     with Pipeline(device=0, chunk_frames=chunk, window=window, depth=depth,
                   threads=threads, max_flows=1 << 12) as p:
@@ -43,6 +48,24 @@ def test_pipeline_matches_oracle(gpu, oracle, window, chunk, depth, threads):
         check_same(res, oracle.parse(t), p.flows())
         st = p.stats()
         assert st["frames"] == t.n and st["chunks"] >= t.n // chunk
+
+
+@pytest.mark.parametrize("nt", ["1", "0"])
+def test_pipeline_windows_at_arena_end(gpu, oracle, nt, monkeypatch):
+    """Runts and short frames packed back to back at the very end of the arena: their
+    80-B windows run past arena_len, so the gather falls back to a bounded copy
+    (zero fill past the arena) for exactly those frames."""
+    from tcbee_amd.trace import Trace
+    monkeypatch.setenv("TCBEE_PIPE_NT", nt)
+    t = mixed_trace(5000, seed=21, n_flows=40)
+    rng = np.random.default_rng(3)
+    tail = [t.frame(i)[:int(rng.integers(10, 90))] for i in range(200)]
+    frames = [t.frame(i) for i in range(t.n)] + tail
+    t2 = Trace.from_frames(frames)
+    assert int(t2.offset[-1] + t2.caplen[-1]) == len(t2.arena)
+    with Pipeline(device=0, chunk_frames=1024, window=80, depth=3, threads=4,
+                  max_flows=1 << 12) as p:
+        check_same(p.run(t2), oracle.parse(t2), p.flows())
 
 
 def test_pipeline_whole_frames_byte_budget(gpu, oracle):
