@@ -109,9 +109,12 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     else:
         d_arena, alen, d_off, d_len, d_ts = build_device_trace(torch, n, sizes, kind, n_flows,
                                                                seed, first, stream)
-    # N>1: two output slots, so that step i's flow-table exchange (side stream) overlaps
-    # step i+1's parse (main stream)
-    overlap = multi and os.environ.get("TCBEE_BENCH_OVERLAP", "1") != "0"
+    # N>1, flow-hash shards: disjoint tables, the global-id exchange runs between K2
+    # and K3 (FlowHashExchange; TCBEE_BENCH_EXCHANGE=merge: the general table merge)
+    fhx = multi and flowhash and os.environ.get("TCBEE_BENCH_EXCHANGE", "fhx") == "fhx"
+    # N>1 contiguous shards (every rank sees every flow): the table merge; two output
+    # slots, so that step i's exchange (side stream) overlaps step i+1's parse
+    overlap = multi and not fhx and os.environ.get("TCBEE_BENCH_OVERLAP", "1") != "0"
     nbuf = 2 if overlap else 1
     slots = [{"rec": torch.empty(n * 74 + 64, dtype=torch.uint8, device="cuda"),
               "hash": torch.empty(n, dtype=torch.int32, device="cuda"),
@@ -132,8 +135,13 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     xcap = max(int(1.25 * flows_here) + 4096, 1 << 12)
     p = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=n, max_arena=0,
                                max_flows=cap)
-    merged = om = fm = None
-    if multi:
+    merged = om = fm = fx = None
+    if fhx:
+        from tcbee_amd.dist import FlowHashExchange
+        merged = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=1024,
+                                        max_arena=0, max_flows=world * xcap)
+        fx = FlowHashExchange(p, xcap, gidx)
+    elif multi:
         from tcbee_amd.dist import FlowMerge, OverlappedMerge
         merged = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=1024,
                                         max_arena=0, max_flows=world * xcap)
@@ -150,6 +158,13 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
         k = count[0] % nbuf
         count[0] += 1
         b = slots[k]
+        if fx is not None:
+            b["ctr"].zero_()
+            p.reset_flows(stream=stream, sync=False)
+            fx.step(d_arena, alen, d_off, d_len, d_ts, n, b["rec"], n, b["hash"], b["id"],
+                    b["n"], b["ctr"], stream)
+            dist.all_reduce(b["ctr"])  # global INGRESS/HANDLED/DROPPED
+            return
         if multi:
             if om is not None:
                 om.acquire(k)
@@ -188,11 +203,18 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     nrec = int(last["n"].item())
     if multi and p.flow_count() > xcap:
         raise RuntimeError(f"rank {rank}: {p.flow_count()} flows exceed the exchange cap {xcap}")
-    flows = (merged if merged is not None else p).flows()
+    if fx is not None:
+        # the global table, assembled once after the timed steps (not part of a step)
+        flows = fx.merged_flows(merged, last["n"], n, n_global)
+    else:
+        flows = (merged if merged is not None else p).flows()
     check = {"records": nrec, "flows": int(len(flows)), "status": status,
              "pkts_total": int(flows["pkts"].sum())}
     if multi:
         check["ingress_global"] = int(last["ctr"][0].item())
+        if fx is not None:
+            check["exchange"] = ("flow-hash: first-frame all-gather (8 B x "
+                                 f"{xcap} per rank) + global ids between K2 and K3")
         if om is not None:
             # side-stream span of one step's exchange (RCCL all-gather of the tables,
             # merge, id remap, counter all-reduce), overlapping the next parse

@@ -161,13 +161,20 @@ int tcbee_parse_batch_device(tcbee_ctx* ctx, const tcbee_frames* in_dev,
                              void* stream);
 
 /* Extended outputs of a device-resident parse (ABI 2). */
+#define TCBEE_EX_DEFER_IDS 0x1u  /* stop before K3: see tcbee_parse_finish_device */
 typedef struct tcbee_parse_ex {
     /* [out_cap] u32: for each record written, the batch-local index of the frame
      * it came from (NULL = not written). What a flow-hash shard of a real trace
      * needs to place its flows in the global trace: rejected frames (non-TCP,
      * runts, FILTER_PORT, xdp.rs:37-92) make record k != frame k. */
     uint32_t* out_frame_index;
-    uint64_t  reserved[7];   /* zero */
+    /* TCBEE_EX_DEFER_IDS: records, hashes and the flow table (with local dense ids)
+     * are produced; the per-record flow ids, pkts/bytes, counters and out_n are
+     * written by tcbee_parse_finish_device, which must come before any other call
+     * on the context. */
+    uint32_t  flags;
+    uint32_t  reserved32;    /* zero */
+    uint64_t  reserved[6];   /* zero */
 } tcbee_parse_ex;
 int tcbee_parse_batch_device_ex(tcbee_ctx* ctx, const tcbee_frames* in_dev,
                                 const tcbee_cfg* cfg,
@@ -175,6 +182,12 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* ctx, const tcbee_frames* in_dev,
                                 uint32_t* out_flow_hash, uint32_t* out_flow_id,
                                 uint64_t* out_n_dev, tcbee_counters* ctr_dev,
                                 const tcbee_parse_ex* ex, void* stream);
+
+/* Completes a TCBEE_EX_DEFER_IDS parse (K3): out_flow_id[p] = id_map_dev[local
+ * id of record p's flow] (0xFFFFFFFF past map_len), or the local id when id_map_dev
+ * is NULL; counters by local id, out_n and ctr as the plain call. Asynchronous. */
+int tcbee_parse_finish_device(tcbee_ctx* ctx, const uint32_t* id_map_dev, uint64_t map_len,
+                              void* stream);
 
 /* Same, host buffers in and out (H2D of frames, D2H of records), synchronous.
  * out_n / ctr are host pointers; ctr is accumulated into. */
@@ -225,6 +238,21 @@ int tcbee_flow_export_global_device(tcbee_ctx* ctx, tcbee_flow_entry* out_dev, u
                                     uint64_t* n_dev, const uint32_t* rec_frame_dev,
                                     const uint64_t* frame_gidx_dev, uint64_t n_frames,
                                     uint64_t rec_frame_cap, void* stream);
+/* The flow-hash exchange: tables of the ranks are disjoint, so
+ * global first-seen ids need only each flow's global first frame.
+ * first_frames: out_first_frame_dev[local id] = global frame index of the flow's
+ * first record (placed as tcbee_flow_export_global_device places it; same
+ * TCBEE_ESHARD rule), n_dev[0] = the context's flows (capped at cap).
+ * global_ids: from the all-gathered arrays (rank r's at all_first_frame_dev +
+ * r*stride, its count at all_n_dev[r]) the local -> global id map of `rank`:
+ * out_map_dev[l] = l + flows of other ranks whose first frame comes earlier. */
+int tcbee_flow_first_frames_device(tcbee_ctx* ctx, uint64_t* out_first_frame_dev, uint64_t cap,
+                                   uint64_t* n_dev, const uint32_t* rec_frame_dev,
+                                   const uint64_t* frame_gidx_dev, uint64_t n_frames,
+                                   uint64_t rec_frame_cap, void* stream);
+int tcbee_global_ids_device(const uint64_t* all_first_frame_dev, const uint64_t* all_n_dev,
+                            uint32_t world, uint32_t rank, uint64_t stride, uint32_t* out_map_dev,
+                            uint64_t map_cap, void* stream);
 /* After merging global-order exports, first_seen of the merged table is a global
  * FRAME index; the reference's is the global RECORD index (accepted frames
  * before it). This rank's share: out_counts_dev[id] = number of this rank's

@@ -65,8 +65,12 @@ class FlowEntry(C.Structure):
                 ("bytes", C.c_uint64), ("first_seen", C.c_uint64)]
 
 
+EX_DEFER_IDS = 0x1
+
+
 class ParseEx(C.Structure):
-    _fields_ = [("out_frame_index", C.c_void_p), ("reserved", C.c_uint64 * 7)]
+    _fields_ = [("out_frame_index", C.c_void_p), ("flags", C.c_uint32),
+                ("reserved32", C.c_uint32), ("reserved", C.c_uint64 * 6)]
 
 
 class PipeCfg(C.Structure):
@@ -102,6 +106,12 @@ _SIGS = {
                                               C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                               C.c_void_p, C.c_void_p, C.POINTER(ParseEx),
                                               C.c_void_p]),
+    "tcbee_parse_finish_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    "tcbee_flow_first_frames_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64,
+                                                 C.c_void_p, C.c_void_p, C.c_void_p,
+                                                 C.c_uint64, C.c_uint64, C.c_void_p]),
+    "tcbee_global_ids_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                          C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]),
     "tcbee_parse_batch": (C.c_int, [C.c_void_p, C.POINTER(Frames), C.POINTER(Cfg),
                                     C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                     C.POINTER(C.c_uint64), C.POINTER(Counters)]),

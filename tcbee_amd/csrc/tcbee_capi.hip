@@ -66,6 +66,12 @@ struct tcbee_ctx {
   uint32_t* d_mbprefix = nullptr;
   uint64_t m_words = 0;
 
+  // deferred K3 (TCBEE_EX_DEFER_IDS): launched by tcbee_parse_finish_device
+  bool count_pending = false;
+  CountArgs pend{};
+  unsigned pend_g1 = 0, pend_g1s = 0, pend_g2 = 0;
+  uint32_t* d_omap = nullptr;  // composed claim -> output id (allocated on first use)
+
   // K1 timing (tcbee_ctx_profile)
   bool profiling = false;
   std::vector<hipEvent_t> ev;  // pairs
@@ -182,6 +188,7 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
   dfree(c->d_mbitmap);
   dfree(c->d_mwprefix);
   dfree(c->d_mbprefix);
+  dfree(c->d_omap);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -327,10 +334,14 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
                                 uint32_t* out_flow_id, uint64_t* out_n_dev,
                                 tcbee_counters* ctr_dev, const tcbee_parse_ex* ex, void* stream) {
   if (!c || !in || !cfg) return TCBEE_EINVAL;
+  if (c->count_pending) return TCBEE_EINVAL;  // tcbee_parse_finish_device first
   uint32_t* out_frame = ex ? ex->out_frame_index : nullptr;
-  if (ex)
+  const bool defer = ex && (ex->flags & TCBEE_EX_DEFER_IDS);
+  if (ex) {
+    if (ex->flags & ~TCBEE_EX_DEFER_IDS || ex->reserved32) return TCBEE_EINVAL;
     for (uint64_t r : ex->reserved)
       if (r) return TCBEE_EINVAL;
+  }
   if (out_frame && in->n > 0xFFFFFFFFull) return TCBEE_EINVAL;  // u32 frame indices
   if (cfg->direction > 1) return TCBEE_EINVAL;
   if (in->n > c->max_frames) return TCBEE_ECAPACITY;
@@ -412,6 +423,7 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     k.batch = c->d_batch;
     k.persist = c->d_persist;
     k.cmap = c->tab.cmap;
+    k.omap = c->tab.cmap;
     k.bitmap = c->d_bitmap;
     k.cnt = c->tab.cnt;
     k.part = c->d_count_part;
@@ -432,11 +444,70 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     uint64_t g1s = (in->n + 8191) / 8192;
     if (g1s > 2ull * c->n_cu) g1s = 2ull * c->n_cu;
     if (g1s == 0) g1s = 1;
+    if (defer) {
+      c->pend = k;
+      c->pend_g1 = (unsigned)g1;
+      c->pend_g1s = (unsigned)g1s;
+      c->pend_g2 = c->d_k3_region ? c->k3_g2 : 0u;
+      c->count_pending = true;
+      return TCBEE_OK;
+    }
     TRY_HIP(launch_count(k, (unsigned)g1, (unsigned)g1s, c->d_k3_region ? c->k3_g2 : 0u, s,
                          c->k3_variant));
   } else {
     TRY_HIP(launch_finalize(c->d_batch, c->d_persist, out_cap, out_n_dev, ctr_dev, cfg->direction, s));
   }
+  return TCBEE_OK;
+}
+
+int tcbee_parse_finish_device(tcbee_ctx* c, const uint32_t* id_map_dev, uint64_t map_len,
+                              void* stream) {
+  if (!c || !c->count_pending || (map_len && !id_map_dev)) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  CountArgs k = c->pend;
+  if (id_map_dev) {
+    if (!c->d_omap) TRY_HIP(dalloc(&c->d_omap, c->nslots));
+    TRY_HIP(launch_compose(c->tab.cmap, id_map_dev, map_len, c->d_batch, c->d_omap, c->nslots, s));
+    k.omap = c->d_omap;
+  }
+  c->count_pending = false;
+  TRY_HIP(launch_count(k, c->pend_g1, c->pend_g1s, c->pend_g2, s, c->k3_variant));
+  return TCBEE_OK;
+}
+
+int tcbee_flow_first_frames_device(tcbee_ctx* c, uint64_t* out_first_frame_dev, uint64_t cap,
+                                   uint64_t* n_dev, const uint32_t* rec_frame_dev,
+                                   const uint64_t* frame_gidx_dev, uint64_t n_frames,
+                                   uint64_t rec_frame_cap, void* stream) {
+  if (!c || (cap && !out_first_frame_dev) || (n_frames && !frame_gidx_dev)) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (int rc = apply_pending_reset(c, s)) return rc;
+  GlobalExportArgs g{};
+  g.tab = c->tab;
+  g.out = out_first_frame_dev;
+  g.cap = cap;
+  g.persist = c->d_persist;
+  g.batch = c->d_batch;
+  g.n_out = n_dev;
+  g.rec_frame = rec_frame_dev;
+  g.frame_gidx = frame_gidx_dev;
+  g.n_frames = n_frames;
+  g.out_cap = rec_frame_dev ? rec_frame_cap : ~0ull;
+  TRY_HIP(launch_first_frames(g, s));
+  return TCBEE_OK;
+}
+
+int tcbee_global_ids_device(const uint64_t* all_first_frame_dev, const uint64_t* all_n_dev,
+                            uint32_t world, uint32_t rank, uint64_t stride, uint32_t* out_map_dev,
+                            uint64_t map_cap, void* stream) {
+  if (!all_first_frame_dev || !all_n_dev || world == 0 || rank >= world ||
+      (map_cap && !out_map_dev))
+    return TCBEE_EINVAL;
+  if (!stride || !map_cap) return TCBEE_OK;
+  TRY_HIP(launch_global_ids(all_first_frame_dev, all_n_dev, world, rank, stride, out_map_dev,
+                            map_cap, (hipStream_t)stream));
   return TCBEE_OK;
 }
 

@@ -113,7 +113,9 @@ struct CountArgs {
   uint64_t out_cap;
   const BatchState* batch;
   const PersistState* persist;
-  const uint32_t* cmap;      // claim index -> dense id
+  const uint32_t* cmap;      // claim index -> local dense id (counters)
+  const uint32_t* omap;      // claim index -> output id written to out_id (cmap, or
+                             // cmap composed with a local -> global id map)
   uint32_t* bitmap;          // first-seen bitmap: words [0, fs_max_word] cleared here
   uint64_t* cnt;
   uint64_t* part;            // mode 0: [g1][kCountBins] per-block packed bins
@@ -168,6 +170,14 @@ hipError_t launch_records_before(FlowTable t, const uint32_t* rec_frame,
 // first_seen of flow id := fs_by_id[id] (ids < cap)
 hipError_t launch_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t cap,
                                  hipStream_t s);
+// Flow-hash exchange: first frame per local id (GlobalExportArgs.out = u64[cap]);
+// global ids from the all-gathered first-frame arrays; output-id composition.
+hipError_t launch_first_frames(const GlobalExportArgs& g, hipStream_t s);
+hipError_t launch_global_ids(const uint64_t* allG, const uint64_t* alln, uint32_t world,
+                             uint32_t rank, uint64_t stride, uint32_t* gid, uint64_t cap,
+                             hipStream_t s);
+hipError_t launch_compose(const uint32_t* cmap, const uint32_t* id_map, uint64_t map_len,
+                          const BatchState* b, uint32_t* omap, uint64_t max_flows, hipStream_t s);
 hipError_t launch_merge(const MergeArgs& g, const RankArgs& r, hipStream_t s);
 hipError_t launch_remap(uint32_t* ids, uint64_t n_max, const uint64_t* n_dev, const uint32_t* map,
                         uint64_t map_len, hipStream_t s);

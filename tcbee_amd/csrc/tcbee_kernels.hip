@@ -1211,7 +1211,7 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
     if (!(SABL & 4)) {
       uint32_t id[U];
 #pragma unroll
-      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.cmap[s[k]];
+      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.omap[s[k]];
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
@@ -1271,11 +1271,14 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
 }
 
 // ABL3 (timing-only ablations, 0 in every product launch): 1 no bin updates,
-// 2 no id gather, 4 no id stores
+// 2 no id gather, 4 no id stores.
+// Bins are indexed by CLAIM (dense in [0, F)); the record's output id is
+// omap[claim] (the local dense id, or — after a flow-hash exchange — the global
+// one), staged in LDS; k_count_reduce maps claims to local ids for the counters.
 template <int U, int ABL3, bool PACK>
 __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
-  __shared__ uint64_t s_bin[kCountBins];
-  __shared__ uint32_t s_map[kCountBins];  // claim index -> dense id
+  __shared__ uint64_t s_bin[kCountBins];  // by claim
+  __shared__ uint32_t s_map[kCountBins];  // claim index -> output id
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint64_t n_acc = c.batch->n_acc;
   const uint64_t nflows = c.batch->flow_total;
@@ -1307,13 +1310,15 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   if (mode == 0) {
     for (uint32_t b = tid; b < nflows; b += kCountBlock) {
       s_bin[b] = 0;
-      s_map[b] = c.cmap[b];
+      s_map[b] = c.omap[b];
     }
     __syncthreads();
   }
-  auto global_add = [&](uint32_t id, uint64_t pk, uint64_t by) {
-    atomicAdd((unsigned long long*)&c.cnt[2ull * id], (unsigned long long)pk);
-    atomicAdd((unsigned long long*)&c.cnt[2ull * id + 1], (unsigned long long)by);
+  // counters are kept by LOCAL dense id
+  auto global_add = [&](uint32_t claim, uint64_t pk, uint64_t by) {
+    const uint32_t lid = c.cmap[claim];
+    atomicAdd((unsigned long long*)&c.cnt[2ull * lid], (unsigned long long)pk);
+    atomicAdd((unsigned long long*)&c.cnt[2ull * lid + 1], (unsigned long long)by);
   };
   for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
     uint32_t s[U], len[U], id[U];
@@ -1326,7 +1331,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
       for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : s_map[s[k]];
     } else {
 #pragma unroll
-      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.cmap[s[k]];
+      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.omap[s[k]];
     }
     if (c.out_id && !(ABL3 & 4)) {
 #pragma unroll
@@ -1344,13 +1349,13 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
     }
     if (mode == 0) {
       // one flow in all of the wave's records this iteration (a hot flow): one add
-      const uint32_t id0 = __builtin_amdgcn_readfirstlane(id[0]);
-      bool same = id0 != 0xFFFFFFFFu;
+      const uint32_t s0 = __builtin_amdgcn_readfirstlane(s[0]);
+      bool same = s0 != 0xFFFFFFFFu;
       uint32_t nk = 0, sl = 0;
 #pragma unroll
       for (int k = 0; k < U; ++k) {
-        const bool v = id[k] != 0xFFFFFFFFu;
-        same = same && (!v || (id[k] == id0 && len[k] < kBigLen));
+        const bool v = s[k] != 0xFFFFFFFFu;
+        same = same && (!v || (s[k] == s0 && len[k] < kBigLen));
         nk += v ? 1u : 0u;
         sl += v ? len[k] : 0u;
       }
@@ -1358,29 +1363,29 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
         // pk <= 64*U, by <= 64*U*(kBigLen-1) < 2^32
         const uint32_t pk = wave_sum32(nk), by = wave_sum32(sl);
         if (lane == 0)
-          atomicAdd((unsigned long long*)&s_bin[id0], ((unsigned long long)pk << kBinPkShift) | by);
+          atomicAdd((unsigned long long*)&s_bin[s0], ((unsigned long long)pk << kBinPkShift) | by);
       } else {
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-          if (id[k] == 0xFFFFFFFFu) continue;
+          if (s[k] == 0xFFFFFFFFu) continue;
           if (len[k] < kBigLen)
-            atomicAdd((unsigned long long*)&s_bin[id[k]], (1ull << kBinPkShift) | len[k]);
+            atomicAdd((unsigned long long*)&s_bin[s[k]], (1ull << kBinPkShift) | len[k]);
           else
-            global_add(id[k], 1, len[k]);
+            global_add(s[k], 1, len[k]);
         }
       }
     } else {
 #pragma unroll
       for (int k = 0; k < U; ++k) {
-        const bool mine = id[k] != 0xFFFFFFFFu;
+        const bool mine = s[k] != 0xFFFFFFFFu;
         const uint64_t am = __ballot(mine);
         const uint32_t leader = am ? (uint32_t)__ffsll((unsigned long long)am) - 1 : 0u;
-        const uint32_t id0 = __shfl(id[k], leader);
-        if (__all(!mine || id[k] == id0)) {
+        const uint32_t s0 = __shfl(s[k], leader);
+        if (__all(!mine || s[k] == s0)) {
           const uint64_t bs = wave_sum64(mine ? (uint64_t)len[k] : 0ull);
-          if (am && lane == leader) global_add(id0, (uint64_t)__popcll(am), bs);
+          if (am && lane == leader) global_add(s0, (uint64_t)__popcll(am), bs);
         } else if (mine) {
-          global_add(id[k], 1, len[k]);
+          global_add(s[k], 1, len[k]);
         }
       }
     }
@@ -1480,9 +1485,10 @@ __global__ void k_count_reduce(CountArgs c, uint32_t g1, uint32_t g2) {
         pk += v >> kBinPkShift;
         by += v & kBinByMask;
       }
-      if (pk) {
-        c.cnt[2 * f] += pk;
-        c.cnt[2 * f + 1] += by;
+      if (pk) {  // rows are by claim; counters by local dense id
+        const uint32_t id = c.cmap[f];
+        c.cnt[2ull * id] += pk;
+        c.cnt[2ull * id + 1] += by;
       }
     }
   } else if (mode == 1) {
@@ -1623,6 +1629,79 @@ __global__ void k_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t
     if (m[0] < 2 || m[7] == 0) continue;
     const uint64_t id = m[7] - 1;
     if (id < cap) m[6] = fs_by_id[id];
+  }
+}
+
+// Flow-hash exchange (disjoint per-rank tables): per local id, the
+// global frame index of the flow's first record (same placement rules as
+// k_export_global), for the cheap global-id exchange.
+__global__ void k_first_frames(GlobalExportArgs g) {
+  const uint64_t nslots = g.tab.mask + 1;
+  const uint64_t hi = g.persist->rec_base, nacc = g.batch->n_acc, lo = hi - nacc;
+  const bool identity = g.rec_frame == nullptr;
+  const bool bad_batch = identity && nacc != g.n_frames;
+  bool bad = false;
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < nslots;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t* m = g.tab.meta + 8 * s;
+    if (m[0] < 2 || m[7] == 0) continue;
+    const uint64_t id = m[7] - 1;
+    if (id >= g.cap) continue;
+    const uint64_t fs = m[6];
+    uint64_t gfs = ~0ull;
+    if (fs >= lo && fs < hi && fs - lo < g.out_cap && !bad_batch) {
+      const uint64_t r = fs - lo;
+      const uint64_t fr = identity ? r : g.rec_frame[r];
+      if (fr < g.n_frames) gfs = g.frame_gidx[fr];
+    }
+    bad = bad || gfs == ~0ull;
+    g.out[id] = gfs;
+  }
+  if (__any(bad) && __lane_id() == 0) atomicOr(&g.persist->status, kStShard);
+  if (g.n_out && blockIdx.x == 0 && threadIdx.x == 0) {
+    g.n_out[0] = g.persist->flow_count < g.cap ? g.persist->flow_count : g.cap;
+    if (bad_batch) atomicOr(&g.persist->status, kStShard);
+  }
+}
+
+// gid[l] = l + (flows of the other ranks first seen before flow l of this rank):
+// each rank's first-frame array is ascending in its local ids (local ids are in
+// local first-seen order, a subsequence of the global trace), so a binary search
+// per other rank counts them; flows are disjoint across ranks, frames distinct.
+__global__ void k_global_ids(const uint64_t* allG, const uint64_t* alln, uint32_t world,
+                             uint32_t rank, uint64_t stride, uint32_t* gid, uint64_t cap) {
+  const uint64_t mine = alln[rank] < stride ? alln[rank] : stride;
+  for (uint64_t l = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; l < mine && l < cap;
+       l += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t G = allG[(uint64_t)rank * stride + l];
+    uint64_t id = l;
+    for (uint32_t r = 0; r < world; ++r) {
+      if (r == rank) continue;
+      const uint64_t* A = allG + (uint64_t)r * stride;
+      uint64_t lo = 0, len = alln[r] < stride ? alln[r] : stride;
+      while (len > 0) {
+        const uint64_t half = len >> 1;
+        if (A[lo + half] < G) {
+          lo += half + 1;
+          len -= half + 1;
+        } else {
+          len = half;
+        }
+      }
+      id += lo;
+    }
+    gid[l] = (uint32_t)id;
+  }
+}
+
+// omap[claim] = id_map[cmap[claim]] for this batch's flows (output ids of K3)
+__global__ void k_compose(const uint32_t* cmap, const uint32_t* id_map, uint64_t map_len,
+                          const BatchState* b, uint32_t* omap) {
+  const uint64_t n = b->flow_total;
+  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < n;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t l = cmap[c];
+    omap[c] = l < map_len ? id_map[l] : 0xFFFFFFFFu;
   }
 }
 
@@ -2013,6 +2092,27 @@ hipError_t launch_records_before(FlowTable t, const uint32_t* rec_frame, const u
 
 hipError_t launch_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t cap, hipStream_t s) {
   hipLaunchKernelGGL(k_set_first_seen, dim3(grid_for(t.mask + 1)), dim3(kBlock), 0, s, t, fs_by_id, cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_first_frames(const GlobalExportArgs& g, hipStream_t s) {
+  hipLaunchKernelGGL(k_first_frames, dim3(grid_for(g.tab.mask + 1)), dim3(kBlock), 0, s, g);
+  return hipGetLastError();
+}
+
+hipError_t launch_global_ids(const uint64_t* allG, const uint64_t* alln, uint32_t world,
+                             uint32_t rank, uint64_t stride, uint32_t* gid, uint64_t cap,
+                             hipStream_t s) {
+  const uint64_t n = stride < cap ? stride : cap;
+  hipLaunchKernelGGL(k_global_ids, dim3(grid_for(n)), dim3(kBlock), 0, s, allG, alln, world, rank,
+                     stride, gid, cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_compose(const uint32_t* cmap, const uint32_t* id_map, uint64_t map_len,
+                          const BatchState* b, uint32_t* omap, uint64_t max_flows, hipStream_t s) {
+  hipLaunchKernelGGL(k_compose, dim3(grid_for(max_flows)), dim3(kBlock), 0, s, cmap, id_map, map_len,
+                     b, omap);
   return hipGetLastError();
 }
 

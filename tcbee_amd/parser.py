@@ -133,24 +133,31 @@ class PacketParser:
                      out_rec, out_cap: int, out_hash=None, out_id=None, out_n=None,
                      counters=None, filter_port: int = 0,
                      direction: int = _lib.DIR_INGRESS, flows: bool = True,
-                     stream: int | None = None, out_frame=None) -> None:
+                     stream: int | None = None, out_frame=None, defer_ids: bool = False) -> None:
         """Asynchronous parse of frames already in HBM (pointers or torch tensors).
 
         out_n: device u64[1]; counters: device u64[4] (accumulated); out_frame:
-        device u32[out_cap], the batch-local frame index of each record."""
+        device u32[out_cap], the batch-local frame index of each record; defer_ids:
+        stop before K3 (finish_device writes ids, pkts/bytes, counters, out_n)."""
         fr = _lib.Frames(_ptr(arena), arena_len, _ptr(offset), _ptr(caplen), _ptr(ts_ns), n)
         cfg = _lib.Cfg(filter_port, direction, 0, 0 if flows else _lib.F_NO_FLOWS)
-        if out_frame is None:
+        if out_frame is None and not defer_ids:
             _lib.check(_lib.lib().tcbee_parse_batch_device(
                 self._h, C.byref(fr), C.byref(cfg), _ptr(out_rec), C.c_uint64(out_cap),
                 _ptr(out_hash), _ptr(out_id), _ptr(out_n), _ptr(counters),
                 C.c_void_p(stream or 0)), "tcbee_parse_batch_device")
             return
-        ex = _lib.ParseEx(_ptr(out_frame))
+        ex = _lib.ParseEx(_ptr(out_frame), _lib.EX_DEFER_IDS if defer_ids else 0)
         _lib.check(_lib.lib().tcbee_parse_batch_device_ex(
             self._h, C.byref(fr), C.byref(cfg), _ptr(out_rec), C.c_uint64(out_cap),
             _ptr(out_hash), _ptr(out_id), _ptr(out_n), _ptr(counters), C.byref(ex),
             C.c_void_p(stream or 0)), "tcbee_parse_batch_device_ex")
+
+    def finish_device(self, id_map=None, map_len: int = 0, stream: int | None = None) -> None:
+        """K3 of a defer_ids parse: out_id = id_map[local id] (or the local id)."""
+        _lib.check(_lib.lib().tcbee_parse_finish_device(
+            self._h, _ptr(id_map), C.c_uint64(map_len if id_map is not None else 0),
+            C.c_void_p(stream or 0)), "tcbee_parse_finish_device")
 
     # -- measurement --------------------------------------------------------------
     def profile(self, enable: bool = True) -> None:
@@ -204,6 +211,16 @@ class PacketParser:
             self._h, _ptr(out), C.c_uint64(cap), _ptr(meta), _ptr(rec_frame), _ptr(frame_gidx),
             C.c_uint64(n_frames), C.c_uint64(rec_frame_cap), C.c_void_p(stream or 0)),
             "tcbee_flow_export_global_device")
+
+    def first_frames_device(self, out, cap: int, n_dev, frame_gidx, n_frames: int,
+                            rec_frame=None, rec_frame_cap: int = 0,
+                            stream: int | None = None) -> None:
+        """out[local id] = global frame index of the flow's first record; n_dev[0] =
+        flows (the flow-hash exchange's per-rank input)."""
+        _lib.check(_lib.lib().tcbee_flow_first_frames_device(
+            self._h, _ptr(out), C.c_uint64(cap), _ptr(n_dev), _ptr(rec_frame), _ptr(frame_gidx),
+            C.c_uint64(n_frames), C.c_uint64(rec_frame_cap), C.c_void_p(stream or 0)),
+            "tcbee_flow_first_frames_device")
 
     def records_before_device(self, rec_frame, frame_gidx, n_rec_dev, n_rec_max: int,
                               out_counts, cap: int, stream: int | None = None) -> None:
@@ -285,6 +302,17 @@ def remap_ids_device(ids, n_max: int, n_dev, id_map, map_len: int,
     _lib.check(_lib.lib().tcbee_remap_ids_device(
         _ptr(ids), C.c_uint64(n_max), _ptr(n_dev), _ptr(id_map), C.c_uint64(map_len),
         C.c_void_p(stream or 0)), "tcbee_remap_ids_device")
+
+
+def global_ids_device(all_first, all_n, world: int, rank: int, stride: int, out_map,
+                      map_cap: int, stream: int | None = None) -> None:
+    """Local -> global flow ids of `rank` from the all-gathered first-frame arrays."""
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream().cuda_stream
+    _lib.check(_lib.lib().tcbee_global_ids_device(
+        _ptr(all_first), _ptr(all_n), world, rank, C.c_uint64(stride), _ptr(out_map),
+        C.c_uint64(map_cap), C.c_void_p(stream or 0)), "tcbee_global_ids_device")
 
 
 def flow_hash64(key40: bytes) -> int:

@@ -112,6 +112,9 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode, n_flows=3000, filter_po
     from tcbee_amd.dist import FlowMerge, OverlappedMerge, shard_range
     from tracegen import mixed_trace
 
+    fhx = mode.startswith("fhx")  # FlowHashExchange instead of FlowMerge
+    if fhx:
+        mode = "flowhash" + mode[3:]
     gidx = None
     if mode == "flowhash":
         import bench
@@ -133,7 +136,7 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode, n_flows=3000, filter_po
         off = torch.from_numpy(sub.offset.view(np.int64)).cuda()
         ln = torch.from_numpy(sub.caplen.view(np.int32)).cuda()
         ts = torch.from_numpy(sub.ts_ns.view(np.int64)).cuda()
-    with_frame = mode == "flowhash_real"
+    with_frame = mode == "flowhash_real"  # (fhx_real too: the prefix was rewritten)
     nbuf = 2 if mode == "overlap" else 1
     slots = [{"rec": torch.empty(m * 74 + 64, dtype=torch.uint8, device="cuda"),
               "hash": torch.empty(m, dtype=torch.int32, device="cuda"),
@@ -145,34 +148,52 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode, n_flows=3000, filter_po
     status = 0
     with tcbee_amd.PacketParser(max_frames=max(m, 1), max_flows=cap) as p, \
             tcbee_amd.PacketParser(max_frames=1024, max_flows=world * cap) as mg:
-        fm = FlowMerge(p, mg, cap, n, nbuf=nbuf)
-        fm.gidx = gidx
-        om = OverlappedMerge(fm, nbuf=nbuf) if mode == "overlap" else None
-        steps = 3 if om else 1
-        for i in range(steps):
-            k = i % nbuf
-            b = slots[k]
-            if om:
-                om.acquire(k)
-            b["ctr"].zero_()
-            p.reset_flows(stream=s, sync=False)
-            p.parse_device(arena, alen, off, ln, ts, m, b["rec"], m, b["hash"], b["id"],
-                           b["n"], b["ctr"], stream=s, filter_port=filter_port,
-                           out_frame=b["frame"])
-            if om:
-                om.submit(k, b["id"], b["n"], m, ctr=b["ctr"])
-            else:
-                fm.step(b["id"], b["n"], m, stream=s, rec_frame=b["frame"])
+        if fhx:
+            from tcbee_amd.dist import FlowHashExchange
+            fx = FlowHashExchange(p, cap, gidx if gidx is not None
+                                  else torch.arange(m, dtype=torch.int64, device="cuda"))
+            steps = 2  # the second step re-uses every buffer of the first
+            for i in range(steps):
+                b = slots[0]
+                b["ctr"].zero_()
+                p.reset_flows(stream=s, sync=False)
+                fx.step(arena, alen, off, ln, ts, m, b["rec"], m, b["hash"], b["id"], b["n"],
+                        b["ctr"], s, filter_port=filter_port, rec_frame=b["frame"])
                 dist.all_reduce(b["ctr"])
-        torch.cuda.synchronize()
-        status = p.status()
-        b = slots[(steps - 1) % nbuf]
+            torch.cuda.synchronize()
+            status = p.status()
+            merged = fx.merged_flows(mg, b["n"], m, n, rec_frame=b["frame"])
+            b = slots[0]
+        else:
+            fm = FlowMerge(p, mg, cap, n, nbuf=nbuf)
+            fm.gidx = gidx
+            om = OverlappedMerge(fm, nbuf=nbuf) if mode == "overlap" else None
+            steps = 3 if om else 1
+            for i in range(steps):
+                k = i % nbuf
+                b = slots[k]
+                if om:
+                    om.acquire(k)
+                b["ctr"].zero_()
+                p.reset_flows(stream=s, sync=False)
+                p.parse_device(arena, alen, off, ln, ts, m, b["rec"], m, b["hash"], b["id"],
+                               b["n"], b["ctr"], stream=s, filter_port=filter_port,
+                               out_frame=b["frame"])
+                if om:
+                    om.submit(k, b["id"], b["n"], m, ctr=b["ctr"])
+                else:
+                    fm.step(b["id"], b["n"], m, stream=s, rec_frame=b["frame"])
+                    dist.all_reduce(b["ctr"])
+            torch.cuda.synchronize()
+            status = p.status()
+            merged = mg.flows()
+            b = slots[(steps - 1) % nbuf]
         k = int(b["n"].item())
         np.savez(os.path.join(result_dir, f"rank{rank}.npz"),
                  gidx=(gidx.cpu().numpy() if gidx is not None else np.zeros(0, np.int64)),
                  rec=b["rec"][:k * 74].cpu().numpy().reshape(-1, 74),
                  gids=b["id"][:k].cpu().numpy().view(np.uint32),
-                 ctr=b["ctr"].cpu().numpy(), merged=mg.flows().view(np.uint8),
+                 ctr=b["ctr"].cpu().numpy(), merged=merged.view(np.uint8),
                  status=np.array([status]))
     dist.barrier()
     dist.destroy_process_group()

@@ -68,7 +68,8 @@ def test_gpu_world2_flowhash_shards(gpu, oracle, tmp_path):
         assert int(x["ctr"][0]) == ctr["ingress"]
 
 
-def test_gpu_world2_flowhash_200k_flows(gpu, oracle, tmp_path):
+@pytest.mark.parametrize("exchange", ["flowhash", "fhx"])
+def test_gpu_world2_flowhash_200k_flows(gpu, oracle, tmp_path, exchange):
     """the flow-hash partition at >= 200k flows (each rank's table
     ~125k flows, K3's bucketed large-table mode, the records-before first_seen
     fix-up over 600k global frames)."""
@@ -79,7 +80,7 @@ def test_gpu_world2_flowhash_200k_flows(gpu, oracle, tmp_path):
     from tcbee_amd.parser import FLOW_DTYPE
     n, flows, world = 600_000, 250_000, 2
     cap = int(1.25 * flows / world) + 4096
-    mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path), "flowhash",
+    mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path), exchange,
                                         flows), nprocs=world, join=True)
     tr = tcbee_amd.synth_trace(n, sizes="imix", kind=1, n_flows=flows)
     ft = oracle.new_flowtab(1 << 19)
@@ -100,8 +101,9 @@ def test_gpu_world2_flowhash_200k_flows(gpu, oracle, tmp_path):
         assert int(x["ctr"][0]) == ctr["ingress"] and int(x["status"][0]) == 0
 
 
+@pytest.mark.parametrize("exchange", ["flowhash_real", "fhx_real"])
 @pytest.mark.parametrize("filter_port", [0, 5201])
-def test_gpu_world2_flowhash_real_trace(gpu, oracle, tmp_path, filter_port):
+def test_gpu_world2_flowhash_real_trace(gpu, oracle, tmp_path, filter_port, exchange):
     """VERDICT r1 #2 / ADVICE r1: flow-hash shards of a REAL trace (non-TCP frames,
     runts, IPv6, v4-compatible collisions, FILTER_PORT) — record k of a rank is not
     its frame k. The host partitioner (the NIC-RSS step) splits the trace; each
@@ -116,7 +118,7 @@ def test_gpu_world2_flowhash_real_trace(gpu, oracle, tmp_path, filter_port):
     from tcbee_amd.parser import FLOW_DTYPE
     n, flows, cap, world = 200_000, 5000, 8192, 2
     mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path),
-                                        "flowhash_real", flows, filter_port),
+                                        exchange, flows, filter_port),
              nprocs=world, join=True)
     tr = mixed_trace(n, seed=404, n_flows=flows)
     rec, fh, fi, ctr, table = oracle.parse(tr, filter_port=filter_port)
@@ -151,7 +153,7 @@ def test_gpu_world2_flowhash_without_frame_map_is_refused(gpu, tmp_path):
         assert int(np.load(tmp_path / f"rank{r}.npz")["status"][0]) == _lib.ESHARD
 
 
-@pytest.mark.parametrize("mode", ["overlap", "flowhash_real"])
+@pytest.mark.parametrize("mode", ["overlap", "flowhash_real", "fhx_real"])
 def test_gpu_rccl_world1_exchange(gpu, oracle, tmp_path, mode):
     """The RCCL branch of the exchange (all_gather_into_tensor + all_reduce on the
     `nccl` backend, i.e. RCCL) on this one-GPU box: world 1, since RCCL refuses two
@@ -162,10 +164,10 @@ def test_gpu_rccl_world1_exchange(gpu, oracle, tmp_path, mode):
     from tracegen import mixed_trace
     from tcbee_amd.parser import FLOW_DTYPE
     n, flows, cap = 60_000, 700, 2048
+    fp = 5201 if mode.endswith("_real") else 0
     mp.spawn(dist_worker.run_gpu, args=(1, free_port(), n, cap, str(tmp_path), mode, flows,
-                                        5201 if mode == "flowhash_real" else 0, "nccl"),
+                                        fp, "nccl"),
              nprocs=1, join=True)
-    fp = 5201 if mode == "flowhash_real" else 0
     tr = mixed_trace(n, seed=404, n_flows=flows)
     rec, fh, fi, ctr, table = oracle.parse(tr, filter_port=fp)
     x = np.load(tmp_path / "rank0.npz")

@@ -30,7 +30,11 @@ for s in "$@"; do
     rccl1)  step rccl1 600 env TCBEE_BENCH_FORCE_MERGE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29537 bench.py --config4 --steps 5 --warmup 2 --no-cpu --no-extra ;;
     dist2c4) step dist2c4 600 env TCBEE_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29539 bench.py --gpus 2 --config4 --frames 30000000 --steps 3 --warmup 1 ;;
     c4v8)   step c4v8 600 python bench.py --config4 --virtual-world 8 --steps 10 --warmup 2 --no-cpu --no-extra --sample-check ;;
+    rccl1m) step rccl1m 600 env TCBEE_BENCH_FORCE_MERGE=1 TCBEE_BENCH_EXCHANGE=merge python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29545 bench.py --config4 --steps 5 --warmup 2 --no-cpu --no-extra ;;
+    rccl3)  step rccl3 600 env TCBEE_BENCH_FORCE_MERGE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29547 bench.py --shard flowhash --steps 20 --warmup 3 --no-cpu --no-extra --sample-check ;;
     capsweep) step capsweep 900 python tools/k1_sweep.py --fpl 2 --flows-only --workloads imix10k,imix125k,imix1M --frames 100000000 --rounds 2 --iters 3 --cap-mult 1,4,8,16 ;;
+    smallprof) step smallprof 600 bash tools/small_prof.sh ;;
+    xprof)  step xprof 600 env MASTER_ADDR=127.0.0.1 MASTER_PORT=29543 RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 TCBEE_BENCH_FORCE_MERGE=1 rocprofv3 --kernel-trace --stats -d gpurun_out/xprof -o run --output-format csv -- python bench.py --config4 --steps 5 --warmup 1 --no-cpu --no-extra --sample-check ;;
     sq)     step sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS --output-format csv -d gpurun_out/sq -o run -- python tools/k1_sweep.py --rounds 1 --iters 2 --fpl 2 --workloads imix10k ;;
     prof)   step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --no-cpu --no-extra --sample-check ;;
     c4prof) step c4prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/c4prof -o run --output-format csv -- python bench.py --config4 --virtual-world 8 --steps 5 --warmup 1 --no-cpu --no-extra --sample-check ;;
