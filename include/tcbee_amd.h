@@ -171,7 +171,8 @@ typedef struct tcbee_parse_ex {
     /* TCBEE_EX_DEFER_IDS: records, hashes and the flow table (with local dense ids)
      * are produced; the per-record flow ids, pkts/bytes, counters and out_n are
      * written by tcbee_parse_finish_device, which must come before any other call
-     * on the context. */
+     * on the context except tcbee_flow_first_frames_device (the exchange's input;
+     * tcbee_flow_export_global_device also places flows then, without counts). */
     uint32_t  flags;
     uint32_t  reserved32;    /* zero */
     uint64_t  reserved[6];   /* zero */

@@ -495,6 +495,7 @@ int tcbee_flow_first_frames_device(tcbee_ctx* c, uint64_t* out_first_frame_dev, 
   g.frame_gidx = frame_gidx_dev;
   g.n_frames = n_frames;
   g.out_cap = rec_frame_dev ? rec_frame_cap : ~0ull;
+  g.k3_pending = c->count_pending;
   TRY_HIP(launch_first_frames(g, s));
   return TCBEE_OK;
 }
@@ -641,6 +642,7 @@ int tcbee_flow_export_global_device(tcbee_ctx* c, tcbee_flow_entry* out_dev, uin
   g.frame_gidx = frame_gidx_dev;
   g.n_frames = n_frames;
   g.out_cap = rec_frame_dev ? rec_frame_cap : ~0ull;
+  g.k3_pending = c->count_pending;
   TRY_HIP(launch_export_global(g, s));
   return TCBEE_OK;
 }

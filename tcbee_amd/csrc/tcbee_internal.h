@@ -160,6 +160,8 @@ struct GlobalExportArgs {
   const uint64_t* frame_gidx;
   uint64_t n_frames;
   uint64_t out_cap;  // records of the batch that have a rec_frame entry
+  bool k3_pending;   // called between K2 and a deferred K3: the persistent record
+                     // base and flow count are not advanced yet
 };
 hipError_t launch_export_global(const GlobalExportArgs& g, hipStream_t s);
 // Merged table (first_seen = global frame index): out[id] = number of this

@@ -1559,7 +1559,10 @@ __global__ void k_export(FlowTable t, uint64_t* out, uint64_t cap, const Persist
 // record that cannot be placed flags kStShard and exports first_seen ~0.
 __global__ void k_export_global(GlobalExportArgs g) {
   const uint64_t nslots = g.tab.mask + 1;
-  const uint64_t hi = g.persist->rec_base, nacc = g.batch->n_acc, lo = hi - nacc;
+  const uint64_t nacc = g.batch->n_acc;
+  const uint64_t lo = g.k3_pending ? g.persist->rec_base : g.persist->rec_base - nacc;
+  const uint64_t hi = lo + nacc;
+  const uint64_t nflows = g.k3_pending ? g.batch->flow_total : g.persist->flow_count;
   const bool identity = g.rec_frame == nullptr;
   const bool bad_batch = identity && nacc != g.n_frames;
   bool bad = false;
@@ -1586,7 +1589,7 @@ __global__ void k_export_global(GlobalExportArgs g) {
   }
   if (__any(bad) && __lane_id() == 0) atomicOr(&g.persist->status, kStShard);
   if (g.n_out && blockIdx.x == 0 && threadIdx.x == 0) {
-    g.n_out[0] = g.persist->flow_count < g.cap ? g.persist->flow_count : g.cap;
+    g.n_out[0] = nflows < g.cap ? nflows : g.cap;
     g.n_out[1] = 0;  // first_seen is already global: the merge rebases nothing
     if (bad_batch) atomicOr(&g.persist->status, kStShard);
   }
@@ -1637,7 +1640,10 @@ __global__ void k_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t
 // k_export_global), for the cheap global-id exchange.
 __global__ void k_first_frames(GlobalExportArgs g) {
   const uint64_t nslots = g.tab.mask + 1;
-  const uint64_t hi = g.persist->rec_base, nacc = g.batch->n_acc, lo = hi - nacc;
+  const uint64_t nacc = g.batch->n_acc;
+  const uint64_t lo = g.k3_pending ? g.persist->rec_base : g.persist->rec_base - nacc;
+  const uint64_t hi = lo + nacc;
+  const uint64_t nflows = g.k3_pending ? g.batch->flow_total : g.persist->flow_count;
   const bool identity = g.rec_frame == nullptr;
   const bool bad_batch = identity && nacc != g.n_frames;
   bool bad = false;
@@ -1659,7 +1665,7 @@ __global__ void k_first_frames(GlobalExportArgs g) {
   }
   if (__any(bad) && __lane_id() == 0) atomicOr(&g.persist->status, kStShard);
   if (g.n_out && blockIdx.x == 0 && threadIdx.x == 0) {
-    g.n_out[0] = g.persist->flow_count < g.cap ? g.persist->flow_count : g.cap;
+    g.n_out[0] = nflows < g.cap ? nflows : g.cap;
     if (bad_batch) atomicOr(&g.persist->status, kStShard);
   }
 }
