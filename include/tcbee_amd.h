@@ -282,6 +282,11 @@ int tcbee_flow_reset_device(tcbee_ctx* ctx, void* stream);
  * Synchronous; clears the status. */
 int tcbee_ctx_status(tcbee_ctx* ctx);
 
+/* Diagnostic: how the last batch's per-flow counting (K3) ran — 0 LDS bins per
+ * block, 1 claims bucketed, 2 device atomics, 3 claim ranges per XCD column,
+ * -1 none yet. Synchronous. */
+int tcbee_ctx_count_mode(tcbee_ctx* ctx, int* mode);
+
 /* ---- measurement ------------------------------------------------------------
  * When enabled, every parse call records a HIP event pair around K1 (the parse
  * kernel) on the stream it is launched on. profile_read synchronizes those

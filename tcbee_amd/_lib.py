@@ -136,6 +136,7 @@ _SIGS = {
     "tcbee_remap_ids_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                          C.c_uint64, C.c_void_p]),
     "tcbee_ctx_profile": (C.c_int, [C.c_void_p, C.c_int]),
+    "tcbee_ctx_count_mode": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     "tcbee_ctx_profile_read": (C.c_int, [C.c_void_p, C.POINTER(C.c_double),
                                          C.POINTER(C.c_uint64)]),
     "tcbee_gen_frames_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,

@@ -23,6 +23,7 @@ struct tcbee_ctx {
   uint32_t withhold_every = 0;  // TCBEE_TEST_WITHHOLD (look-back recount test hook)
   int k3_no_bucket = 0;         // TCBEE_TEST_K3_NOBUCKET=1: large tables use K3 mode 2 (test hook)
   int k3_variant = 0;           // TCBEE_K3ABL: timing-only K3 ablations / tilings (A/B)
+  bool k3_range = false;        // K3 mode 3 available (part rows sized for it)
   int k1_variant = 0;           // TCBEE_K1V: K1 staging/occupancy A/B variants
   uint32_t plain_walk = kPlainWalk;  // TCBEE_WALK: K1 plain probe walk length (A/B)
   uint32_t pack_bits = 0;            // K1->K3 scratch packing (0: two words per record)
@@ -44,7 +45,7 @@ struct tcbee_ctx {
   uint32_t* d_k3_offs = nullptr;
   uint64_t* d_k3_lpart = nullptr;
   uint32_t k3_nb_max = 0, k3_g2 = 0;
-  uint64_t k3_g1max = 0;
+  uint64_t k3_g1max = 0, part_words = 0;
   int n_cu = 256;
   uint64_t max_words = 0, max_sblocks = 0;
 
@@ -267,7 +268,18 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   // one partial-bin row each
   c->k3_g1max = (max_frames + kK3MaxPer - 1) / kK3MaxPer;
   if (c->k3_g1max < (uint64_t)c->n_cu) c->k3_g1max = c->n_cu;
-  if ((e = dalloc(&c->d_count_part, c->k3_g1max * kCountBins)) != hipSuccess)
+  // (tables past kCountBins slots also hold K3 mode 3's per-group rows: at most
+  //  8 x (g1 / 8 / 2) groups x kRangeFlows claims; TCBEE_TEST_K3_NORANGE=1 keeps
+  //  such tables on modes 1/2 — a test hook)
+  uint64_t part_words = c->k3_g1max * kCountBins;
+  c->k3_range = c->nslots > (uint64_t)kCountBins;
+  if (const char* e = std::getenv("TCBEE_TEST_K3_NORANGE")) c->k3_range = c->k3_range && !std::atoi(e);
+  if (c->k3_range) {
+    const uint64_t rows = (uint64_t)c->n_cu / 2;  // R >= 2 in mode 3: <= g1/16 groups x 8
+    if (rows * kRangeFlows > part_words) part_words = rows * kRangeFlows;
+  }
+  c->part_words = part_words;
+  if ((e = dalloc(&c->d_count_part, part_words)) != hipSuccess)
     return fail(map_err(e));
   if (c->nslots > (uint64_t)kCountBins && !c->k3_no_bucket) {
     // K3 mode 1 scratch: (claim, caplen) per frame, bucket offsets per K3 block,
@@ -427,6 +439,8 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     k.bitmap = c->d_bitmap;
     k.cnt = c->tab.cnt;
     k.part = c->d_count_part;
+    k.range_ok = c->k3_range ? 1u : 0u;
+    k.part_words = c->part_words;
     k.region = c->d_k3_region;
     k.offs = c->d_k3_offs;
     k.nb_max = c->k3_nb_max;
@@ -439,6 +453,15 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     const uint64_t gmin = (in->n + kK3MaxPer - 1) / kK3MaxPer;
     if (g1 < gmin) g1 = gmin;
     if (g1 == 0) g1 = 1;
+    if (c->k3_range) {
+      // mode 3 needs whole XCD columns of R >= 2 blocks: a multiple of 8, >= 128
+      // blocks where the chip has them (each block then covers fewer records)
+      const uint64_t want = (uint64_t)c->n_cu / 8 * 8 < 128 ? (uint64_t)c->n_cu / 8 * 8 : 128;
+      uint64_t g = (g1 + 7) / 8 * 8;
+      if (g < want) g = want;
+      if (g <= c->k3_g1max) g1 = g;
+    }
+    k.g1 = (uint32_t)g1;
     // finalize is folded into k_count's block 0
     // mode-1 scatter: two 1024-thread workgroups per CU (its offsets rows: 2 n_cu)
     uint64_t g1s = (in->n + 8191) / 8192;
@@ -749,6 +772,16 @@ int tcbee_ctx_status(tcbee_ctx* c) {
   if (p.status & kStSpin) return TCBEE_ESPIN;
   if (p.status & kStFlowFull) return TCBEE_EFLOWFULL;
   if (p.status & kStShard) return TCBEE_ESHARD;
+  return TCBEE_OK;
+}
+
+int tcbee_ctx_count_mode(tcbee_ctx* c, int* mode) {
+  if (!c || !mode) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  PersistState p{};
+  TRY_HIP(hipMemcpyAsync(&p, c->d_persist, sizeof(p), hipMemcpyDeviceToHost, c->stream));
+  TRY_HIP(hipStreamSynchronize(c->stream));
+  *mode = (int)p.k3_mode - 1;
   return TCBEE_OK;
 }
 

@@ -35,7 +35,7 @@ struct PersistState {
   uint64_t rec_base;    // accepted frames before this batch
   uint64_t flow_count;  // flows with ids
   uint32_t status;
-  uint32_t pad0;
+  uint32_t k3_mode;     // diagnostic: K3 mode of the last batch + 1 (0: none yet)
   uint64_t pad1;
 };
 
@@ -118,7 +118,11 @@ struct CountArgs {
                              // cmap composed with a local -> global id map)
   uint32_t* bitmap;          // first-seen bitmap: words [0, fs_max_word] cleared here
   uint64_t* cnt;
-  uint64_t* part;            // mode 0: [g1][kCountBins] per-block packed bins
+  uint64_t* part;            // mode 0: [g1][kCountBins] per-block packed bins;
+                             // mode 3: [groups][F] per-group packed bins by claim
+  uint32_t g1;               // k_count's grid (mode 3 eligibility: count_mode)
+  uint32_t range_ok;         // mode 3 allowed (0: test hook / small table)
+  uint64_t part_words;       // capacity of part (u64)
   // mode 1 (large tables; region == nullptr disables it)
   uint32_t* region;          // per accepted frame: claim within its bucket | caplen
                              // << kBucketBits (0 when >= kRegLenEsc: added by a global
@@ -211,6 +215,10 @@ constexpr int kScanWordsPerBlock = 2048;  // 256 threads x 8 words
 constexpr uint64_t kRankSmallWords = 1024 * 32;  // single-block rank up to 1M frames
 constexpr int kCountBlock = 1024;
 constexpr int kCountBins = 12288;         // 96 KiB of u64 bins + 48 KiB claim->id map in LDS
+// K3 mode 3: claims split into R ranges of <= kCountBins, R <= kMaxRanges; the
+// R blocks of a group share one XCD (b % 8) and one record segment
+constexpr uint32_t kMaxRanges = 16;
+constexpr uint64_t kRangeFlows = (uint64_t)kCountBins * kMaxRanges;  // mode 3 up to 196608 flows
 constexpr int kBinPkShift = 40;           // K3 bin: pkts in bits 63:40, bytes in 39:0
 constexpr uint32_t kBigLen = 1u << 16;    // caplen >= 64 KiB: counted by device atomics
 // a K3 block covers at most kK3MaxPer records (a multiple of the range granule),

@@ -1105,16 +1105,31 @@ __global__ void k_assign(RankArgs r) {
 //     aggregated first.
 constexpr uint64_t kBinByMask = (1ull << kBinPkShift) - 1;
 
-__device__ __forceinline__ int count_mode(const CountArgs& c, uint64_t nflows) {
-  if (nflows <= (uint64_t)kCountBins) return 0;
-  if (c.region && nflows <= (uint64_t)c.nb_max * kBucket) return 1;
-  return 2;
-}
-
 // records [lo, hi) of K3 block `b` (identical in k_count and k_count_bucket)
 __device__ __forceinline__ uint64_t count_per(uint64_t n_acc, uint32_t grid) {
   return ((n_acc + grid - 1) / grid + kK3Gran - 1) / kK3Gran * kK3Gran;
 }
+
+// mode 3 geometry from the flow count: R ranges, groups per XCD column
+__device__ __forceinline__ uint32_t range_count(uint64_t nflows) {
+  return (uint32_t)((nflows + kCountBins - 1) / kCountBins);
+}
+__device__ __forceinline__ uint32_t range_groups_per_x(const CountArgs& c, uint64_t nflows) {
+  return (c.g1 / 8u) / range_count(nflows);
+}
+
+__device__ __forceinline__ int count_mode(const CountArgs& c, uint64_t nflows) {
+  if (nflows <= (uint64_t)kCountBins) return 0;
+  // mode 3: every group of R blocks re-reads its segment R times (from the XCD's
+  // L2); a group must cover < kK3MaxPer records (bin fields cannot overflow)
+  if (c.range_ok && nflows <= kRangeFlows && c.g1 % 8u == 0 && range_groups_per_x(c, nflows) > 0 &&
+      count_per(c.batch->n_acc, 8u * range_groups_per_x(c, nflows)) <= kK3MaxPer &&
+      8ull * range_groups_per_x(c, nflows) * nflows <= c.part_words)
+    return 3;
+  if (c.region && nflows <= (uint64_t)c.nb_max * kBucket) return 1;
+  return 2;
+}
+
 
 // K1's per-record scratch of U accepted records p0 + k*kCountBlock (p < hi;
 // others give claim ~0, len 0): claim (~0: no flow) and caplen, packed in one
@@ -1270,6 +1285,80 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
   }
 }
 
+// Mode 3 (kCountBins < F <= kRangeFlows): the claims are split into R ranges of
+// at most kCountBins; block b works for range r of group g, where the R blocks of a
+// group share b % 8 — one XCD under the observed round-robin placement (speed only)
+// — and one contiguous record segment. Each block streams its group's segment
+// (after the first of the R readers, from that XCD's L2), keeps only the records
+// whose claim lies in its range: output id from the range's map in LDS (written
+// where it lands: the R blocks fill each out_id line between them), pkts/bytes
+// into the range's LDS bins; one partial row per group, summed by the reduce.
+// Replaces the bucket scatter's two passes + region round trip and the per-record
+// claim -> id gather from L2 (mode 1) for the sizes one GPU's flow-hash share of
+// config 4 has (~125k flows).
+template <int U, bool PACK>
+__device__ void count_ranges(const CountArgs& c, uint64_t n_acc, uint64_t nflows,
+                             uint64_t* s_bin, uint32_t* s_map) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t R = range_count(nflows), px = range_groups_per_x(c, nflows);
+  const uint32_t b = blockIdx.x, x = b % 8u, j = b / 8u;
+  const uint32_t gx = j / R, r = j % R;
+  if (gx >= px) return;
+  const uint32_t G = 8u * px, g = gx * 8u + x;
+  const uint64_t per = count_per(n_acc, G);
+  const uint64_t lo = (uint64_t)g * per < n_acc ? (uint64_t)g * per : n_acc;
+  const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
+  const uint64_t width = (nflows + R - 1) / R;  // <= kCountBins
+  const uint64_t c0 = (uint64_t)r * width;
+  const uint64_t c1 = c0 + width < nflows ? c0 + width : nflows;
+  const uint32_t nb = c1 > c0 ? (uint32_t)(c1 - c0) : 0u;
+  for (uint32_t i = tid; i < nb; i += kCountBlock) {
+    s_bin[i] = 0;
+    s_map[i] = c.omap[c0 + i];
+  }
+  __syncthreads();
+  for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
+    uint32_t v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
+      v[k] = __builtin_nontemporal_load(&c.acc_flow[p < hi ? p : lo]);
+      if (p >= hi) v[k] = 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint32_t cl = (PACK && v[k] != 0xFFFFFFFFu) ? (v[k] & ((1u << c.pack_bits) - 1u)) : v[k];
+      const uint32_t rel = cl - (uint32_t)c0;  // wraps for claims below the range
+      const bool hit = cl != 0xFFFFFFFFu && rel < nb;
+      if (!__any(hit)) continue;
+      const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
+      uint32_t len = 0;
+      if (hit) {
+        len = PACK ? v[k] >> c.pack_bits : c.acc_len[p];
+        if (PACK && len == (0xFFFFFFFFu >> c.pack_bits)) len = c.acc_len[p];  // saturated
+        if (c.out_id && p < c.out_cap) c.out_id[p] = s_map[rel];
+      }
+      // a hot flow: every lane of the wave on one claim -> one LDS add
+      const uint32_t r0 = __builtin_amdgcn_readfirstlane(rel);
+      if (__all(hit && rel == r0 && len < kBigLen)) {
+        const uint32_t by = wave_sum32(len);
+        if (lane == 0) atomicAdd((unsigned long long*)&s_bin[r0], (64ull << kBinPkShift) | by);
+      } else if (hit) {
+        if (len < kBigLen) {
+          atomicAdd((unsigned long long*)&s_bin[rel], (1ull << kBinPkShift) | len);
+        } else {
+          const uint32_t lid = c.cmap[cl];  // counters by local id
+          atomicAdd((unsigned long long*)&c.cnt[2ull * lid], 1ull);
+          atomicAdd((unsigned long long*)&c.cnt[2ull * lid + 1], (unsigned long long)len);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  uint64_t* part = c.part + (uint64_t)g * nflows + c0;
+  for (uint32_t i = tid; i < nb; i += kCountBlock) part[i] = s_bin[i];
+}
+
 // ABL3 (timing-only ablations, 0 in every product launch): 1 no bin updates,
 // 2 no id gather, 4 no id stores.
 // Bins are indexed by CLAIM (dense in [0, F)); the record's output id is
@@ -1303,10 +1392,15 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
       c.bitmap[w] = 0;
   }
   const int mode = count_mode(c, nflows);
+  if (blockIdx.x == 0 && tid == 0) c.persist_rw->k3_mode = (uint32_t)mode + 1u;
   const uint64_t per = count_per(n_acc, gridDim.x);
   const uint64_t lo = (uint64_t)blockIdx.x * per < n_acc ? (uint64_t)blockIdx.x * per : n_acc;
   const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
   if (mode == 1) return;  // k_count_scatter
+  if (mode == 3) {
+    count_ranges<U, PACK>(c, n_acc, nflows, s_bin, s_map);
+    return;
+  }
   if (mode == 0) {
     for (uint32_t b = tid; b < nflows; b += kCountBlock) {
       s_bin[b] = 0;
@@ -1486,6 +1580,21 @@ __global__ void k_count_reduce(CountArgs c, uint32_t g1, uint32_t g2) {
         by += v & kBinByMask;
       }
       if (pk) {  // rows are by claim; counters by local dense id
+        const uint32_t id = c.cmap[f];
+        c.cnt[2ull * id] += pk;
+        c.cnt[2ull * id + 1] += by;
+      }
+    }
+  } else if (mode == 3) {
+    const uint32_t G = 8u * range_groups_per_x(c, nflows);
+    for (uint64_t f = t0; f < nflows; f += stride) {
+      uint64_t pk = 0, by = 0;
+      for (uint32_t g = 0; g < G; ++g) {
+        const uint64_t v = c.part[(uint64_t)g * nflows + f];
+        pk += v >> kBinPkShift;
+        by += v & kBinByMask;
+      }
+      if (pk) {
         const uint32_t id = c.cmap[f];
         c.cnt[2ull * id] += pk;
         c.cnt[2ull * id + 1] += by;
@@ -2066,7 +2175,7 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
     hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1s);
   }
   // mode 0 needs kCountBins threads; mode 1 up to nb_max * kBucket (grid-stride)
-  const unsigned gr = g2 ? 1024u : (unsigned)(kCountBins / 256);
+  const unsigned gr = (g2 || c.range_ok) ? 1024u : (unsigned)(kCountBins / 256);
   hipLaunchKernelGGL(k_count_reduce, dim3(gr), dim3(256), 0, s, c, g1, g2);  // g1: mode-0 rows
   return hipGetLastError();
 }

@@ -159,6 +159,12 @@ class PacketParser:
             self._h, _ptr(id_map), C.c_uint64(map_len if id_map is not None else 0),
             C.c_void_p(stream or 0)), "tcbee_parse_finish_device")
 
+    def count_mode(self) -> int:
+        """K3 mode of the last batch (0 bins, 1 buckets, 2 atomics, 3 claim ranges)."""
+        m = C.c_int(-1)
+        _lib.check(_lib.lib().tcbee_ctx_count_mode(self._h, C.byref(m)), "tcbee_ctx_count_mode")
+        return m.value
+
     # -- measurement --------------------------------------------------------------
     def profile(self, enable: bool = True) -> None:
         _lib.check(_lib.lib().tcbee_ctx_profile(self._h, int(enable)), "tcbee_ctx_profile")

@@ -239,14 +239,17 @@ def test_lookback_recount_fallback(gpu, oracle, every, monkeypatch):
         assert p.status() == 0
 
 
-@pytest.mark.parametrize("mode", ["bucket", "atomic"])
+@pytest.mark.parametrize("mode", ["range", "bucket", "atomic"])
 @pytest.mark.parametrize("n,flows", [(300_000, 30_000), (200_000, 13_000), (120_000, 100_000)])
 def test_k3_large_table_modes(gpu, oracle, mode, n, flows, monkeypatch):
-    """More flows than K3's LDS bins (12288): mode 1 (claims bucketed per block,
-    per-bucket LDS histograms, claim->id in the reduce) and mode 2 (device atomics,
-    TCBEE_TEST_K3_NOBUCKET) both exact, over two batches (claims of batch 1 looked
-    up again in batch 2)."""
+    """More flows than K3's LDS bins (12288): mode 3 (claim ranges, one LDS map +
+    bins per range, where the grid has the XCD columns for it; else mode 1), mode 1
+    (claims bucketed per block, per-bucket LDS histograms; TCBEE_TEST_K3_NORANGE)
+    and mode 2 (device atomics, + TCBEE_TEST_K3_NOBUCKET) all exact, over two
+    batches (claims of batch 1 looked up again in batch 2)."""
     from tracegen import mixed_trace
+    if mode in ("bucket", "atomic"):
+        monkeypatch.setenv("TCBEE_TEST_K3_NORANGE", "1")
     if mode == "atomic":
         monkeypatch.setenv("TCBEE_TEST_K3_NOBUCKET", "1")
     tr = mixed_trace(n, seed=97, n_flows=flows)
@@ -260,6 +263,8 @@ def test_k3_large_table_modes(gpu, oracle, mode, n, flows, monkeypatch):
         fl = p.flows()
         assert len(fl) == len(table) and np.array_equal(fl, table)
         assert p.status() == 0
+        if mode != "range":
+            assert p.count_mode() == (1 if mode == "bucket" else 2)
 
 
 @pytest.mark.parametrize("nopack", ["0", "1"])
@@ -453,3 +458,49 @@ def test_config4_1M_flows_device_right_sized(gpu, oracle):
         assert np.array_equal(fi_d.cpu().numpy().view(np.uint32), fi)
         assert np.array_equal(p.flows(), table)
         assert p.status() == 0
+
+
+@pytest.mark.parametrize("pool,n", [(10_500, 1_500_000), (75_000, 2_500_000),
+                                    (98_000, 3_000_000)])
+def test_k3_range_mode_large_batches(gpu, oracle, pool, n):
+    """K3 mode 3 at 2, 12 and 16 claim ranges (the config-4 per-GPU share has ~125k
+    flows): a mixed trace with hot, rejected and > 64 KiB frames; ids, the whole table
+    and counters vs the oracle, device-resident, one batch."""
+    import torch
+    from tracegen import mixed_trace
+    tr = mixed_trace(n, seed=pool, n_flows=pool)  # ~1.9 distinct keys per pool flow
+    ln = tr.caplen.copy()
+    rng = np.random.default_rng(7)
+    big = rng.choice(tr.n - 1, size=50, replace=False)
+    pad = 200_000
+    arena = np.concatenate([tr.arena, np.zeros(pad, np.uint8)])
+    ln[big] = np.uint32(70_000)  # caplen past the LDS bins' 64 KiB: device atomics
+    tr = Trace(arena, tr.offset, ln, tr.ts_ns)
+    d_arena = torch.from_numpy(np.concatenate([tr.arena, np.zeros(64, np.uint8)])).cuda()
+    d_off = torch.from_numpy(tr.offset.view(np.int64)).cuda()
+    d_len = torch.from_numpy(tr.caplen.view(np.int32)).cuda()
+    d_ts = torch.from_numpy(tr.ts_ns.view(np.int64)).cuda()
+    rec_d = torch.empty(n * 74 + 64, dtype=torch.uint8, device="cuda")
+    fi_d = torch.empty(n, dtype=torch.int32, device="cuda")
+    n_d = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctr_d = torch.zeros(4, dtype=torch.int64, device="cuda")
+    with tcbee_amd.PacketParser(max_frames=n, max_flows=8 * pool) as p:
+        s = torch.cuda.current_stream().cuda_stream
+        p.parse_device(d_arena, len(tr.arena), d_off, d_len, d_ts, n, rec_d, n, None, fi_d, n_d,
+                       ctr_d, stream=s)
+        torch.cuda.synchronize()
+        ft = oracle.new_flowtab(1 << 19)
+        try:
+            rec, fh, fi, ctr, _ = oracle.parse(tr, ft=ft)
+            table = oracle.flows(ft)
+        finally:
+            oracle.free_flowtab(ft)
+        k = int(n_d.item())
+        assert k == len(rec) and 12288 < len(table) <= 16 * 12288
+        assert np.array_equal(fi_d[:k].cpu().numpy().view(np.uint32), fi)
+        assert np.array_equal(rec_d[:k * 74].cpu().numpy().reshape(-1, 74), rec)
+        assert np.array_equal(p.flows(), table)
+        assert ctr_d.cpu().numpy().tolist() == [ctr["ingress"], ctr["egress"], ctr["handled"],
+                                                 ctr["dropped"]]
+        assert p.status() == 0
+        assert p.count_mode() == 3
