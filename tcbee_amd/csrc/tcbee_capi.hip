@@ -441,6 +441,7 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     k.part = c->d_count_part;
     k.range_ok = c->k3_range ? 1u : 0u;
     k.part_words = c->part_words;
+    k.scatter_unstaged = c->k3_variant == 90 ? 1u : 0u;  // TCBEE_K3ABL=90: A/B
     k.region = c->d_k3_region;
     k.offs = c->d_k3_offs;
     k.nb_max = c->k3_nb_max;

@@ -123,6 +123,7 @@ struct CountArgs {
   uint32_t g1;               // k_count's grid (mode 3 eligibility: count_mode)
   uint32_t range_ok;         // mode 3 allowed (0: test hook / small table)
   uint64_t part_words;       // capacity of part (u64)
+  uint32_t scatter_unstaged; // mode 1 always by the lane-scattered pass 2 (A/B hook)
   // mode 1 (large tables; region == nullptr disables it)
   uint32_t* region;          // per accepted frame: claim within its bucket | caplen
                              // << kBucketBits (0 when >= kRegLenEsc: added by a global
@@ -216,8 +217,11 @@ constexpr uint64_t kRankSmallWords = 1024 * 32;  // single-block rank up to 1M f
 constexpr int kCountBlock = 1024;
 constexpr int kCountBins = 12288;         // 96 KiB of u64 bins + 48 KiB claim->id map in LDS
 // K3 mode 3: claims split into R ranges of <= kCountBins, R <= kMaxRanges; the
-// R blocks of a group share one XCD (b % 8) and one record segment
-constexpr uint32_t kMaxRanges = 16;
+// R blocks of a group share one XCD (b % 8) and one record segment. Every record
+// is visited R times, so it pays only for small R: vs mode 1 at 100M records
+// (tools/k1_sweep.py, TCBEE_TEST_K3_NORANGE A/B) -0.36 ms at 20k flows (R 2),
+// -0.08 at 30k (R 3), +0.12 at 45k (R 4), +0.42 at 60k, +2.8 at 125k (R 11)
+constexpr uint32_t kMaxRanges = 3;
 constexpr uint64_t kRangeFlows = (uint64_t)kCountBins * kMaxRanges;  // mode 3 up to 196608 flows
 constexpr int kBinPkShift = 40;           // K3 bin: pkts in bits 63:40, bytes in 39:0
 constexpr uint32_t kBigLen = 1u << 16;    // caplen >= 64 KiB: counted by device atomics
@@ -227,6 +231,9 @@ constexpr uint64_t kK3Gran = 16384;
 constexpr uint64_t kK3MaxPer = (1ull << 24) - kK3Gran;
 constexpr int kBucketBits = 12, kBucket = 1 << kBucketBits;  // claims per mode-1 bucket
 constexpr uint32_t kMaxBuckets = 4096;    // mode 1 up to 16M flows (hist + cursors: 32 KiB)
+// mode 1 with <= kSmallNb buckets (2M flows): each chunk's entries are
+// counting-sorted in LDS and stored as runs, not scattered lane by lane
+constexpr uint32_t kSmallNb = 512;
 constexpr uint64_t kMaxTableFlows = 1ull << 24;  // tcbee_ctx_create's max_flows limit
 // mode-1 region entry: caplens from kRegLenEsc up are stored as 0 and their bytes
 // added to the flow's counter by a global atomic (frames of >= 1 MiB: never on a

@@ -1202,9 +1202,20 @@ __device__ __forceinline__ uint32_t block1024_excl_scan(uint32_t v, uint32_t* s_
 // Mode 1, phase 1 (inside k_count): ids out, bucket counts, scan, scatter.
 // SABL (timing-only ablations, 0 in product launches): 1 no region stores,
 // 2 no second pass, 4 no id gather/stores in the first pass
-template <int U, bool PACK, int SABL = 0>
+// STAGED (nb <= kSmallNb): pass 2 counting-sorts each chunk of U x 1024 entries
+// by bucket in LDS (stage / sb / ch / co) and stores them as per-bucket runs.
+struct ScatterStage {
+  uint32_t* stage;  // [U * kCountBlock] entries of one chunk, bucket-sorted
+  uint16_t* sb;     // their buckets
+  uint32_t* ch;     // [kSmallNb + 1] chunk counts per bucket (+ spare)
+  uint32_t* co;     // [kSmallNb + 1] chunk offsets per bucket
+};
+
+template <int U, bool PACK, int SABL = 0, bool STAGED = false>
 __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint64_t nflows,
-                              uint32_t* hist, uint32_t* cur, uint32_t* s_w) {
+                              uint32_t* hist, uint32_t* cur, uint32_t* s_w,
+                              const ScatterStage& st = ScatterStage{}) {
+  constexpr uint32_t kMaxBuckets = STAGED ? kSmallNb : tcbee::kMaxBuckets;  // the spare slot
   const uint32_t tid = threadIdx.x;
   const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);
   // Cost at 125M records, 31 buckets (tools/k3_ablate.sh): claim stream 0.09 ms,
@@ -1259,6 +1270,51 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
   if (tid == 0) offs[nb] = total;
   __syncthreads();
   if (SABL & 2) return;
+  if constexpr (STAGED) {
+    for (uint32_t b = tid; b <= kMaxBuckets; b += kCountBlock) st.ch[b] = 0;
+    __syncthreads();
+    for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
+      uint32_t sc[U], len[U], lp[U];
+      load_acc<U, PACK>(c, base + tid, lo, hi, sc, len);
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        lp[k] = atomicAdd(&st.ch[sc[k] != 0xFFFFFFFFu ? (sc[k] >> kBucketBits) : kMaxBuckets], 1u);
+      __syncthreads();
+      // chunk offsets (buckets 0..nb-1; no-flow entries in the spare are dropped)
+      // and each bucket's global base for this chunk, from the block's cursors
+      {
+        const uint32_t v = tid < nb ? st.ch[tid] : 0u;
+        uint32_t tot;
+        const uint32_t off = block1024_excl_scan(v, s_w, tot);
+        if (tid < nb) {
+          st.co[tid] = off;
+          hist[tid] = cur[tid];  // hist (pass-1 counts, done with) = chunk base
+          cur[tid] += v;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        if (sc[k] == 0xFFFFFFFFu) continue;
+        const uint32_t b = sc[k] >> kBucketBits;
+        const uint32_t idx = st.co[b] + lp[k];
+        st.stage[idx] = (sc[k] & (kBucket - 1u)) | ((len[k] < kRegLenEsc ? len[k] : 0u) << kBucketBits);
+        st.sb[idx] = (uint16_t)b;
+        if (len[k] >= kRegLenEsc)
+          atomicAdd((unsigned long long*)&c.cnt[2ull * c.cmap[sc[k]] + 1], (unsigned long long)len[k]);
+      }
+      __syncthreads();
+      const uint32_t nval = nb ? st.co[nb - 1] + st.ch[nb - 1] : 0u;
+      for (uint32_t idx = tid; idx < nval; idx += kCountBlock) {
+        const uint32_t b = st.sb[idx];
+        c.region[lo + hist[b] + (idx - st.co[b])] = st.stage[idx];  // runs: coalesced
+      }
+      __syncthreads();
+      for (uint32_t b = tid; b <= kMaxBuckets; b += kCountBlock) st.ch[b] = 0;
+      __syncthreads();
+    }
+    return;
+  }
   for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
     uint32_t s[U], len[U], pos[U];
     load_acc<U, PACK>(c, base + tid, lo, hi, s, len);
@@ -1501,11 +1557,33 @@ __global__ __launch_bounds__(kCountBlock) void k_count_scatter(CountArgs c) {
   __shared__ uint32_t s_w[kCountBlock / 64];
   const uint64_t nflows = c.batch->flow_total;
   if (count_mode(c, nflows) != 1) return;
+  if (!c.scatter_unstaged && ((nflows + kBucket - 1) >> kBucketBits) <= kSmallNb)
+    return;  // k_count_scatter_staged
   const uint64_t n_acc = c.batch->n_acc;
   const uint64_t per = count_per(n_acc, gridDim.x);
   const uint64_t lo = (uint64_t)blockIdx.x * per < n_acc ? (uint64_t)blockIdx.x * per : n_acc;
   const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
   count_scatter<U, PACK, SABL>(c, lo, hi, nflows, s_hist, s_cur, s_w);
+}
+
+// The same for tables of <= kSmallNb buckets, pass 2 staged through LDS: 4 KiB of
+// counters + 48 KiB of chunk staging = 2 workgroups per CU, as the plain kernel.
+template <int U, bool PACK>
+__global__ __launch_bounds__(kCountBlock) void k_count_scatter_staged(CountArgs c) {
+  __shared__ uint32_t s_hist[kSmallNb + 1], s_cur[kSmallNb + 1];
+  __shared__ uint32_t s_ch[kSmallNb + 1], s_co[kSmallNb + 1];
+  __shared__ uint32_t s_stage[U * kCountBlock];
+  __shared__ uint16_t s_sb[U * kCountBlock];
+  __shared__ uint32_t s_w[kCountBlock / 64];
+  const uint64_t nflows = c.batch->flow_total;
+  if (count_mode(c, nflows) != 1) return;
+  if (c.scatter_unstaged || ((nflows + kBucket - 1) >> kBucketBits) > kSmallNb) return;
+  const uint64_t n_acc = c.batch->n_acc;
+  const uint64_t per = count_per(n_acc, gridDim.x);
+  const uint64_t lo = (uint64_t)blockIdx.x * per < n_acc ? (uint64_t)blockIdx.x * per : n_acc;
+  const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
+  ScatterStage st{s_stage, s_sb, s_ch, s_co};
+  count_scatter<U, PACK, 0, true>(c, lo, hi, nflows, s_hist, s_cur, s_w, st);
 }
 
 // Mode 1, phase 2: workgroup (j, s) histograms bucket j over the segments of K3
@@ -2172,6 +2250,9 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
         if (c.pack_bits) hipLaunchKernelGGL((k_count_scatter<8, true>), gs, dim3(kCountBlock), 0, s, c);
         else hipLaunchKernelGGL((k_count_scatter<8, false>), gs, dim3(kCountBlock), 0, s, c);
     }
+    // (each of the two returns at once unless the table's bucket count is its own)
+    if (c.pack_bits) hipLaunchKernelGGL((k_count_scatter_staged<4, true>), gs, dim3(kCountBlock), 0, s, c);
+    else hipLaunchKernelGGL((k_count_scatter_staged<4, false>), gs, dim3(kCountBlock), 0, s, c);
     hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1s);
   }
   // mode 0 needs kCountBins threads; mode 1 up to nb_max * kBucket (grid-stride)
