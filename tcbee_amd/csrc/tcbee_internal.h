@@ -231,9 +231,12 @@ constexpr uint64_t kK3Gran = 16384;
 constexpr uint64_t kK3MaxPer = (1ull << 24) - kK3Gran;
 constexpr int kBucketBits = 12, kBucket = 1 << kBucketBits;  // claims per mode-1 bucket
 constexpr uint32_t kMaxBuckets = 4096;    // mode 1 up to 16M flows (hist + cursors: 32 KiB)
-// mode 1 with <= kSmallNb buckets (2M flows): each chunk's entries are
-// counting-sorted in LDS and stored as runs, not scattered lane by lane
-constexpr uint32_t kSmallNb = 512;
+// mode 1 with kStagedMinNb..kSmallNb buckets (256k..2M flows): each chunk's
+// entries are counting-sorted in LDS and stored as runs, not scattered lane by
+// lane. At 100M records (TCBEE_K3ABL=90 A/B): 1M flows (245 buckets) -0.42 ms;
+// 125k (31) +0.09 and 60k (15) +0.16 ms, where a wave's lanes already hit few
+// bucket cursors and the per-chunk barriers cost more than they save
+constexpr uint32_t kSmallNb = 512, kStagedMinNb = 64;
 constexpr uint64_t kMaxTableFlows = 1ull << 24;  // tcbee_ctx_create's max_flows limit
 // mode-1 region entry: caplens from kRegLenEsc up are stored as 0 and their bytes
 // added to the flow's counter by a global atomic (frames of >= 1 MiB: never on a

@@ -1551,14 +1551,18 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
 
 // Mode 1, phase 1 as its own launch: 32 KiB of LDS, so two workgroups share a CU
 // (k_count's 144 KiB of bins + map allow one).
+__device__ __forceinline__ bool staged_scatter(const CountArgs& c, uint64_t nflows) {
+  const uint64_t nb = (nflows + kBucket - 1) >> kBucketBits;
+  return !c.scatter_unstaged && nb >= kStagedMinNb && nb <= kSmallNb;
+}
+
 template <int U, bool PACK, int SABL = 0>
 __global__ __launch_bounds__(kCountBlock) void k_count_scatter(CountArgs c) {
   __shared__ uint32_t s_hist[kMaxBuckets + 1], s_cur[kMaxBuckets + 1];  // + spare counter
   __shared__ uint32_t s_w[kCountBlock / 64];
   const uint64_t nflows = c.batch->flow_total;
   if (count_mode(c, nflows) != 1) return;
-  if (!c.scatter_unstaged && ((nflows + kBucket - 1) >> kBucketBits) <= kSmallNb)
-    return;  // k_count_scatter_staged
+  if (staged_scatter(c, nflows)) return;  // k_count_scatter_staged
   const uint64_t n_acc = c.batch->n_acc;
   const uint64_t per = count_per(n_acc, gridDim.x);
   const uint64_t lo = (uint64_t)blockIdx.x * per < n_acc ? (uint64_t)blockIdx.x * per : n_acc;
@@ -1566,7 +1570,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count_scatter(CountArgs c) {
   count_scatter<U, PACK, SABL>(c, lo, hi, nflows, s_hist, s_cur, s_w);
 }
 
-// The same for tables of <= kSmallNb buckets, pass 2 staged through LDS: 4 KiB of
+// The same for tables of kStagedMinNb..kSmallNb buckets, pass 2 staged through LDS: 4 KiB of
 // counters + 48 KiB of chunk staging = 2 workgroups per CU, as the plain kernel.
 template <int U, bool PACK>
 __global__ __launch_bounds__(kCountBlock) void k_count_scatter_staged(CountArgs c) {
@@ -1577,7 +1581,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count_scatter_staged(CountArgs 
   __shared__ uint32_t s_w[kCountBlock / 64];
   const uint64_t nflows = c.batch->flow_total;
   if (count_mode(c, nflows) != 1) return;
-  if (c.scatter_unstaged || ((nflows + kBucket - 1) >> kBucketBits) > kSmallNb) return;
+  if (!staged_scatter(c, nflows)) return;
   const uint64_t n_acc = c.batch->n_acc;
   const uint64_t per = count_per(n_acc, gridDim.x);
   const uint64_t lo = (uint64_t)blockIdx.x * per < n_acc ? (uint64_t)blockIdx.x * per : n_acc;

@@ -460,12 +460,13 @@ def test_config4_1M_flows_device_right_sized(gpu, oracle):
         assert p.status() == 0
 
 
-@pytest.mark.parametrize("pool,n", [(10_500, 1_500_000), (75_000, 2_500_000),
-                                    (98_000, 3_000_000)])
+@pytest.mark.parametrize("pool,n", [(10_500, 1_500_000), (17_000, 2_000_000),
+                                    (75_000, 2_500_000), (170_000, 3_000_000)])
 def test_k3_range_mode_large_batches(gpu, oracle, pool, n):
-    """K3 mode 3 at 2, 12 and 16 claim ranges (the config-4 per-GPU share has ~125k
-    flows): a mixed trace with hot, rejected and > 64 KiB frames; ids, the whole table
-    and counters vs the oracle, device-resident, one batch."""
+    """Large-table K3 on one batch, device-resident: mode 3 at 2 and 3 claim ranges,
+    mode 1 beyond (143k flows: 36 buckets, lane-scattered; ~290k flows: 71 buckets,
+    the LDS-staged scatter); a mixed trace with hot, rejected and > 64 KiB frames;
+    ids, the whole table and counters vs the oracle."""
     import torch
     from tracegen import mixed_trace
     tr = mixed_trace(n, seed=pool, n_flows=pool)  # ~1.9 distinct keys per pool flow
@@ -484,23 +485,23 @@ def test_k3_range_mode_large_batches(gpu, oracle, pool, n):
     fi_d = torch.empty(n, dtype=torch.int32, device="cuda")
     n_d = torch.zeros(1, dtype=torch.int64, device="cuda")
     ctr_d = torch.zeros(4, dtype=torch.int64, device="cuda")
-    with tcbee_amd.PacketParser(max_frames=n, max_flows=8 * pool) as p:
+    with tcbee_amd.PacketParser(max_frames=n, max_flows=4 * pool) as p:
         s = torch.cuda.current_stream().cuda_stream
         p.parse_device(d_arena, len(tr.arena), d_off, d_len, d_ts, n, rec_d, n, None, fi_d, n_d,
                        ctr_d, stream=s)
         torch.cuda.synchronize()
-        ft = oracle.new_flowtab(1 << 19)
+        ft = oracle.new_flowtab(1 << 20)
         try:
             rec, fh, fi, ctr, _ = oracle.parse(tr, ft=ft)
             table = oracle.flows(ft)
         finally:
             oracle.free_flowtab(ft)
         k = int(n_d.item())
-        assert k == len(rec) and 12288 < len(table) <= 16 * 12288
+        assert k == len(rec) and 12288 < len(table)
         assert np.array_equal(fi_d[:k].cpu().numpy().view(np.uint32), fi)
         assert np.array_equal(rec_d[:k * 74].cpu().numpy().reshape(-1, 74), rec)
         assert np.array_equal(p.flows(), table)
         assert ctr_d.cpu().numpy().tolist() == [ctr["ingress"], ctr["egress"], ctr["handled"],
                                                  ctr["dropped"]]
         assert p.status() == 0
-        assert p.count_mode() == 3
+        assert p.count_mode() == (3 if len(table) <= 3 * 12288 else 1)
