@@ -129,7 +129,7 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     # the load: at load 1/2 (max_flows = flows, 128 MiB for 1M flows) K1 is 6 %
     # slower at 10k flows, 31 % at 125k and 36 % at 1M; 8x/16x gain < 3 % on K1 and
     # lose it to the bigger per-step table reset (profiles/r02_capsweep.json)
-    cap = max(4 * flows_here, 1 << 12)
+    cap = max(4 * flows_here, 64)
     # (the exchange carries up to xcap entries per rank: a quarter more than the
     # shard's expected flows)
     xcap = max(int(1.25 * flows_here) + 4096, 1 << 12)
@@ -626,6 +626,16 @@ def main():
                 "frames": c4_n, "flows": 1_000_000, "mpkts": round(c4_n * c4_steps / c_el / 1e6, 1),
                 "ms_per_step": round(c_el / c4_steps * 1e3, 4), "k1_ms": round(c_k1, 4),
                 "check": c_chk}
+            # one GPU's share of config 4 under north_star's flow-hash partition at N=8:
+            # rank 0's shard of the 1B-frame trace (~125M frames, ~125k flows), no exchange
+            v_el, v_k1, v_n, v_chk, v_local = run_device(
+                torch, None, 0, 1, c4_n, "imix", 1, 1_000_000, c4_steps, 1, args.seed,
+                flowhash=True, vworld=8)
+            out["config4_flowhash_share_of_8"] = {
+                "frames": v_local, "flows": v_chk.get("flows"),
+                "mpkts": round(v_local * c4_steps / v_el / 1e6, 1),
+                "ms_per_step": round(v_el / c4_steps * 1e3, 4), "k1_ms": round(v_k1, 4),
+                "check": v_chk}
             out["e2e_host"] = host_e2e(args.sizes, kind, args.flows, args.seed,
                                        n=args.e2e_frames)
             out["config5_replay"] = config5_replay(args.seed)

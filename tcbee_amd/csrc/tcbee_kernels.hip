@@ -1641,7 +1641,27 @@ __global__ void k_count_reduce(CountArgs c, uint32_t g1, uint32_t g2) {
   const int mode = count_mode(c, nflows);
   const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  if (mode == 0) {
+  if (mode == 0 && nflows * 64 <= stride) {
+    // few flows (config 2 has one): one wave per flow, its lanes over the rows —
+    // a thread per flow would walk all g1 rows in a dependent-latency chain
+    const uint64_t f = t0 >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    if (f < nflows) {
+      uint64_t pk = 0, by = 0;
+      for (uint32_t b = lane; b < g1; b += 64) {
+        const uint64_t v = c.part[(uint64_t)b * kCountBins + f];
+        pk += v >> kBinPkShift;
+        by += v & kBinByMask;
+      }
+      pk = wave_sum64(pk);
+      by = wave_sum64(by);
+      if (lane == 0 && pk) {
+        const uint32_t id = c.cmap[f];
+        c.cnt[2ull * id] += pk;
+        c.cnt[2ull * id + 1] += by;
+      }
+    }
+  } else if (mode == 0) {
     for (uint64_t f = t0; f < nflows; f += stride) {
       // 8 independent rows per step: the loads of a thread are in flight together
       uint64_t pk = 0, by = 0;
