@@ -45,6 +45,9 @@ def main():
         lines.append("")
     f = os.path.join(OUT, "pmc_fetch", "run_counter_collection.csv")
     w = os.path.join(OUT, "pmc_write", "run_counter_collection.csv")
+    if not os.path.exists(f):  # tools/pmc_c4.sh layout (config-3 leg)
+        f = os.path.join(OUT, "pmc_c3_fetch", "run_counter_collection.csv")
+        w = os.path.join(OUT, "pmc_c3_write", "run_counter_collection.csv")
     if os.path.exists(f) and os.path.exists(w):
         fk = pmc_values(f, "k_parse")
         wk = pmc_values(w, "k_parse")
@@ -66,6 +69,8 @@ def main():
                   "(algorithmic 156 B/frame)", ""]
         for name in ("pmc_fetch", "pmc_write"):
             src = os.path.join(OUT, name, "run_counter_collection.csv")
+            if not os.path.exists(src):
+                src = os.path.join(OUT, name.replace("pmc_", "pmc_c3_"), "run_counter_collection.csv")
             dst = os.path.join(PROF, f"{tag}_{name}.csv")
             with open(src) as fi, open(dst, "w") as fo:
                 rd = csv.DictReader(fi)
@@ -83,9 +88,67 @@ def main():
                   "Command: `rocprofv3 --kernel-trace --stats -- python bench.py --config4 "
                   "--virtual-world 8 --steps 5 --warmup 1 --no-cpu --no-extra --sample-check` "
                   "(rank 0's flow-hash shard of 1B IMIX frames / 8 GPUs: ~125M frames, "
-                  "~125k flows; K3 in its bucketed mode).", "",
+                  "~125k flows).", "",
                   "| kernel | calls | avg us | total % |", "|---|---|---|---|"]
         for r in csv.DictReader(open(c4)):
+            if "tcbee" in r["Name"]:
+                lines.append(f"| `{r['Name'][:70]}` | {r['Calls']} | "
+                             f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} |")
+        lines.append("")
+    legs = {"c3": ("config 3: 100M IMIX frames, 10k flows", ""),
+            "c4": ("config 4, whole 1M-flow trace on one GPU: 125M IMIX frames", "--config4"),
+            "c4v8": ("config 4, one GPU's flow-hash share at N=8: ~125M frames, ~125k flows",
+                     "--config4 --virtual-world 8")}
+    pmc_legs = {}
+    for leg, (what, args) in legs.items():
+        paths = {k: os.path.join(OUT, f"pmc_{leg}_{k}", "run_counter_collection.csv")
+                 for k in ("fetch", "write", "rdreq")}
+        if not all(os.path.exists(x) for x in paths.values()):
+            continue
+        fk = statistics.median(pmc_values(paths["fetch"], "k_parse"))
+        wk = statistics.median(pmc_values(paths["write"], "k_parse"))
+        rd = {}
+        for r in csv.DictReader(open(paths["rdreq"])):
+            if "k_parse" in r["Kernel_Name"]:
+                rd.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+        rd = {k: statistics.median(v) for k, v in rd.items()}
+        frames = 100_000_000 if leg == "c3" else (125_000_000 if leg == "c4" else 124_967_316)
+        fetch, write = fk * 1024 * 2, wk * 1024
+        pmc_legs[leg] = {"workload": what, "command": "bench.py --steps 2 --warmup 1 --no-cpu "
+                         f"--no-extra --sample-check {args}".strip(), "frames": frames,
+                         "fetch_bytes_corrected": fetch, "write_bytes": write,
+                         "read_B_per_frame": round(fetch / frames, 1),
+                         "write_B_per_frame": round(write / frames, 1),
+                         "traffic_B_per_frame": round((fetch + write) / frames, 1),
+                         "rdreq": rd, "rdreq_per_frame": round(rd.get("TCC_EA0_RDREQ_sum", 0) / frames, 3)}
+        for k, src in paths.items():
+            with open(src) as fi, open(os.path.join(PROF, f"{tag}_pmc_{leg}_{k}.csv"), "w") as fo:
+                rdr = csv.DictReader(fi)
+                cols = ["Dispatch_Id", "Kernel_Name", "Grid_Size", "Workgroup_Size",
+                        "LDS_Block_Size", "VGPR_Count", "Counter_Name", "Counter_Value"]
+                wr = csv.writer(fo)
+                wr.writerow(cols)
+                for r in rdr:
+                    if "tcbee" in r["Kernel_Name"]:
+                        wr.writerow([r[c] for c in cols])
+    if pmc_legs:
+        json.dump(pmc_legs, open(os.path.join(PROF, f"{tag}_pmc_legs.json"), "w"), indent=1)
+        lines += ["## k_parse HBM-side traffic per leg (separate --pmc passes; FETCH x2)", "",
+                  "| leg | read B/frame | write B/frame | total B/frame | L2->fabric read requests/frame |",
+                  "|---|---|---|---|---|"]
+        for leg, v in pmc_legs.items():
+            lines.append(f"| {v['workload']} | {v['read_B_per_frame']} | {v['write_B_per_frame']} | "
+                         f"{v['traffic_B_per_frame']} | {v['rdreq_per_frame']} |")
+        lines.append("")
+    small = os.path.join(OUT, "smallprof", "run_kernel_stats.csv")
+    if os.path.exists(small):
+        shutil.copy(small, os.path.join(PROF, f"{tag}_config2_kernel_stats.csv"))
+        lines += ["## config 2 (1M x 64 B, 1 flow)", "",
+                  "Command: `rocprofv3 --kernel-trace --stats -- python tools/k1_sweep.py "
+                  "--frames 1000000 --fpl 2 --workloads 64B1 --rounds 1 --iters 20` "
+                  "(flows on and off variants).", "",
+                  "| kernel | calls | avg us | total % |", "|---|---|---|---|"]
+        for r in csv.DictReader(open(small)):
             if "tcbee" in r["Name"]:
                 lines.append(f"| `{r['Name'][:70]}` | {r['Calls']} | "
                              f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} |")
