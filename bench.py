@@ -116,6 +116,12 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     # slots, so that step i's exchange (side stream) overlaps step i+1's parse
     overlap = multi and not fhx and os.environ.get("TCBEE_BENCH_OVERLAP", "1") != "0"
     nbuf = 2 if overlap else 1
+    # K3 (ids, pkts/bytes, counters) of step i on a side stream beside step i+1's K1
+    # (TCBEE_EX_ASYNC_IDS; not with the contiguous merge, whose export reads the
+    # counters on the main stream right after the parse)
+    ids_side = (torch.cuda.Stream() if os.environ.get("TCBEE_BENCH_ASYNC", "1") != "0"
+                and (not multi or fhx) else None)
+    ids_stream = ids_side.cuda_stream if ids_side is not None else None
     slots = [{"rec": torch.empty(n * 74 + 64, dtype=torch.uint8, device="cuda"),
               "hash": torch.empty(n, dtype=torch.int32, device="cuda"),
               "id": torch.empty(n, dtype=torch.int32, device="cuda"),
@@ -159,11 +165,14 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
         count[0] += 1
         b = slots[k]
         if fx is not None:
-            b["ctr"].zero_()
+            cs = ids_side if ids_side is not None else torch.cuda.current_stream()
+            with torch.cuda.stream(cs):  # the counters live on K3's stream
+                b["ctr"].zero_()
             p.reset_flows(stream=stream, sync=False)
             fx.step(d_arena, alen, d_off, d_len, d_ts, n, b["rec"], n, b["hash"], b["id"],
-                    b["n"], b["ctr"], stream)
-            dist.all_reduce(b["ctr"])  # global INGRESS/HANDLED/DROPPED
+                    b["n"], b["ctr"], stream, ids_stream=ids_stream)
+            with torch.cuda.stream(cs):
+                dist.all_reduce(b["ctr"])  # global INGRESS/HANDLED/DROPPED
             return
         if multi:
             if om is not None:
@@ -171,7 +180,7 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
             b["ctr"].zero_()
         p.reset_flows(stream=stream, sync=False)
         p.parse_device(d_arena, alen, d_off, d_len, d_ts, n, b["rec"], n, b["hash"], b["id"],
-                       b["n"], b["ctr"], stream=stream)
+                       b["n"], b["ctr"], stream=stream, ids_stream=ids_stream)
         if om is not None:
             om.submit(k, b["id"], b["n"], n, ctr=b["ctr"])
         elif fm is not None:  # TCBEE_BENCH_OVERLAP=0: the exchange in line, one stream

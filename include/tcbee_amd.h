@@ -162,6 +162,7 @@ int tcbee_parse_batch_device(tcbee_ctx* ctx, const tcbee_frames* in_dev,
 
 /* Extended outputs of a device-resident parse (ABI 2). */
 #define TCBEE_EX_DEFER_IDS 0x1u  /* stop before K3: see tcbee_parse_finish_device */
+#define TCBEE_EX_ASYNC_IDS 0x2u  /* K3 on ex->ids_stream, beside the next batch     */
 typedef struct tcbee_parse_ex {
     /* [out_cap] u32: for each record written, the batch-local index of the frame
      * it came from (NULL = not written). What a flow-hash shard of a real trace
@@ -175,7 +176,14 @@ typedef struct tcbee_parse_ex {
      * tcbee_flow_export_global_device also places flows then, without counts). */
     uint32_t  flags;
     uint32_t  reserved32;    /* zero */
-    uint64_t  reserved[6];   /* zero */
+    /* TCBEE_EX_ASYNC_IDS: K3 — the per-record flow ids, pkts/bytes, counters and
+     * out_n — runs on ids_stream (a hipStream_t) after this batch's K2, so it can
+     * overlap the next batch's K1 on `stream` (batches alternate two internal
+     * slots for what K3 reads). The context orders what depends on it: the next
+     * batch's K2 and every table read wait for it. The CALLER orders its own
+     * readers of out_flow_id / out_n / counters after ids_stream. */
+    void*     ids_stream;
+    uint64_t  reserved[5];   /* zero */
 } tcbee_parse_ex;
 int tcbee_parse_batch_device_ex(tcbee_ctx* ctx, const tcbee_frames* in_dev,
                                 const tcbee_cfg* cfg,

@@ -66,11 +66,13 @@ class FlowEntry(C.Structure):
 
 
 EX_DEFER_IDS = 0x1
+EX_ASYNC_IDS = 0x2
 
 
 class ParseEx(C.Structure):
     _fields_ = [("out_frame_index", C.c_void_p), ("flags", C.c_uint32),
-                ("reserved32", C.c_uint32), ("reserved", C.c_uint64 * 6)]
+                ("reserved32", C.c_uint32), ("ids_stream", C.c_void_p),
+                ("reserved", C.c_uint64 * 5)]
 
 
 class PipeCfg(C.Structure):

@@ -31,7 +31,17 @@ struct tcbee_ctx {
   FlowTable tab{};
   uint64_t nslots = 0;
   PersistState* d_persist = nullptr;
-  BatchState* d_batch = nullptr;
+  BatchState* d_batch = nullptr;     // = d_batch_slot[slot] of the current batch
+  // two slots of what a batch's K3 reads (batch state, K1 -> K3 scratch), so that
+  // with TCBEE_EX_ASYNC_IDS batch i's K3 (ids stream) runs beside batch i+1's K1;
+  // the second slot is allocated on the first async call
+  BatchState* d_batch_slot[2] = {nullptr, nullptr};
+  uint32_t* d_slot_scratch_s[2] = {nullptr, nullptr};
+  uint32_t* d_len_scratch_s[2] = {nullptr, nullptr};
+  int slot = 0, nslot = 1;
+  hipEvent_t ev_k2 = nullptr, ev_k3 = nullptr, ev_fin = nullptr;
+  bool k3_async = false;        // a K3 is (or may be) running on another stream
+  hipStream_t pend_ids = nullptr;  // deferred + async: the ids stream
   uint64_t* d_tile_status = nullptr;
   uint64_t max_tiles = 0;
   uint64_t* d_new_list = nullptr;
@@ -124,6 +134,16 @@ int ensure_host_path(tcbee_ctx* c) {
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// Ordering against a K3 that runs on another stream (TCBEE_EX_ASYNC_IDS): host
+// reads of the table wait for it; device work on `s` that reads what it writes
+// (counters, ids) is queued behind it.
+hipError_t k3_wait_host(tcbee_ctx* c) {
+  return c->k3_async ? hipEventSynchronize(c->ev_k3) : hipSuccess;
+}
+hipError_t k3_wait_stream(tcbee_ctx* c, hipStream_t s) {
+  return c->k3_async ? hipStreamWaitEvent(s, c->ev_k3, 0) : hipSuccess;
+}
+
 }  // namespace
 
 extern "C" {
@@ -164,7 +184,16 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
   dfree(c->tab.cnt);
   dfree(c->tab.cmap);
   dfree(c->d_persist);
-  dfree(c->d_batch);
+  if (c->k3_async && c->ev_k3) (void)hipEventSynchronize(c->ev_k3);
+  for (int i = 0; i < 2; ++i) {
+    dfree(c->d_batch_slot[i]);
+    if (i) {  // slot 0's scratch is d_slot_scratch / d_len_scratch, freed below
+      dfree(c->d_slot_scratch_s[i]);
+      dfree(c->d_len_scratch_s[i]);
+    }
+  }
+  for (hipEvent_t e : {c->ev_k2, c->ev_k3, c->ev_fin})
+    if (e) (void)hipEventDestroy(e);
   dfree(c->d_tile_status);
   dfree(c->d_new_list);
   dfree(c->d_bitmap);
@@ -250,7 +279,11 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   if ((e = dalloc(&c->tab.cnt, 2 * c->nslots)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.cmap, c->nslots)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_persist, 1)) != hipSuccess) return fail(map_err(e));
-  if ((e = dalloc(&c->d_batch, 1)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->d_batch_slot[0], 1)) != hipSuccess) return fail(map_err(e));
+  c->d_batch = c->d_batch_slot[0];
+  for (hipEvent_t* ev : {&c->ev_k2, &c->ev_k3, &c->ev_fin})
+    if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
+      return fail(map_err(e));
   if ((e = dalloc(&c->d_tile_status, c->max_tiles)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_new_list, c->nslots)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_bitmap, c->max_words)) != hipSuccess) return fail(map_err(e));
@@ -261,6 +294,8 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   if ((e = dalloc(&c->d_bprefix, c->max_sblocks)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_slot_scratch, max_frames)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_len_scratch, max_frames)) != hipSuccess) return fail(map_err(e));
+  c->d_slot_scratch_s[0] = c->d_slot_scratch;
+  c->d_len_scratch_s[0] = c->d_len_scratch;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->n_cu = prop.multiProcessorCount;
@@ -308,6 +343,7 @@ int tcbee_ctx_stream(tcbee_ctx* c, void** stream) {
 int tcbee_ctx_sync(tcbee_ctx* c) {
   if (!c) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
+  TRY_HIP(k3_wait_host(c));
   TRY_HIP(hipStreamSynchronize(c->stream));
   return TCBEE_OK;
 }
@@ -315,6 +351,7 @@ int tcbee_ctx_sync(tcbee_ctx* c) {
 int tcbee_flow_reset(tcbee_ctx* c) {
   if (!c) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
+  TRY_HIP(k3_wait_host(c));
   TRY_HIP(launch_table_init(c->tab, c->stream));
   TRY_HIP(hipMemsetAsync(c->d_persist, 0, sizeof(PersistState), c->stream));
   // also the recovery point after a failed batch: the first-seen bitmap is whole-zero
@@ -349,8 +386,12 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
   if (c->count_pending) return TCBEE_EINVAL;  // tcbee_parse_finish_device first
   uint32_t* out_frame = ex ? ex->out_frame_index : nullptr;
   const bool defer = ex && (ex->flags & TCBEE_EX_DEFER_IDS);
+  const bool async = ex && (ex->flags & TCBEE_EX_ASYNC_IDS);
+  hipStream_t ids_stream = async ? (hipStream_t)ex->ids_stream : nullptr;
   if (ex) {
-    if (ex->flags & ~TCBEE_EX_DEFER_IDS || ex->reserved32) return TCBEE_EINVAL;
+    if (ex->flags & ~(TCBEE_EX_DEFER_IDS | TCBEE_EX_ASYNC_IDS) || ex->reserved32) return TCBEE_EINVAL;
+    if (async && !ids_stream) return TCBEE_EINVAL;
+    if (!async && ex->ids_stream) return TCBEE_EINVAL;
     for (uint64_t r : ex->reserved)
       if (r) return TCBEE_EINVAL;
   }
@@ -364,6 +405,17 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
   const bool flows = (cfg->flags & TCBEE_F_NO_FLOWS) == 0;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   TRY_HIP(hipSetDevice(c->device));
+  if (async && c->nslot < 2) {
+    // first async batch: the second slot (setup, synchronous allocation)
+    TRY_HIP(dalloc(&c->d_batch_slot[1], 1));
+    TRY_HIP(dalloc(&c->d_slot_scratch_s[1], c->max_frames));
+    TRY_HIP(dalloc(&c->d_len_scratch_s[1], c->max_frames));
+    c->nslot = 2;
+  }
+  if (c->nslot == 2) c->slot ^= 1;  // batches alternate slots once two exist
+  c->d_batch = c->d_batch_slot[c->slot];
+  uint32_t* const acc_flow = c->d_slot_scratch_s[c->slot];
+  uint32_t* const acc_len = c->d_len_scratch_s[c->slot];
   const int fpl = c->fpl;
   const uint64_t ntiles = (in->n + tile_frames(fpl) - 1) / tile_frames(fpl);
   const uint64_t nwords = flows && ntiles ? (in->n + 31) / 32 : 0;
@@ -389,8 +441,8 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     a.out_rec = out_rec74;
     a.out_cap = out_cap;
     a.out_hash = flows ? out_flow_hash : nullptr;
-    a.acc_flow = c->d_slot_scratch;
-    a.acc_len = c->d_len_scratch;
+    a.acc_flow = acc_flow;
+    a.acc_len = acc_len;
     a.tile_status = c->d_tile_status;
     a.ntiles = ntiles;
     a.batch = c->d_batch;
@@ -421,15 +473,19 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     r.bprefix = c->d_bprefix;
     r.nwords = nwords;
     r.nblocks = (r.nwords + kScanWordsPerBlock - 1) / kScanWordsPerBlock;
+    r.update_persist = true;
+    // K2 rewrites claim -> id entries, zeroes new ids' counters and the bitmap K3
+    // clears: after the previous batch's K3, wherever that ran
+    TRY_HIP(k3_wait_stream(c, s));
     TRY_HIP(launch_rank(r, s));
     CountArgs k{};
     k.out_n = out_n_dev;
     k.ctr = ctr_dev;
     k.direction = cfg->direction;
     k.persist_rw = c->d_persist;
-    k.acc_flow = c->d_slot_scratch;
+    k.acc_flow = acc_flow;
     k.pack_bits = c->pack_bits;
-    k.acc_len = c->d_len_scratch;
+    k.acc_len = acc_len;
     k.out_id = out_flow_id;
     k.out_cap = out_cap;
     k.batch = c->d_batch;
@@ -473,11 +529,20 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
       c->pend_g1 = (unsigned)g1;
       c->pend_g1s = (unsigned)g1s;
       c->pend_g2 = c->d_k3_region ? c->k3_g2 : 0u;
+      c->pend_ids = ids_stream;
       c->count_pending = true;
       return TCBEE_OK;
     }
-    TRY_HIP(launch_count(k, (unsigned)g1, (unsigned)g1s, c->d_k3_region ? c->k3_g2 : 0u, s,
+    hipStream_t ks = s;
+    if (async) {  // K3 on the ids stream, after K2
+      TRY_HIP(hipEventRecord(c->ev_k2, s));
+      TRY_HIP(hipStreamWaitEvent(ids_stream, c->ev_k2, 0));
+      ks = ids_stream;
+    }
+    TRY_HIP(launch_count(k, (unsigned)g1, (unsigned)g1s, c->d_k3_region ? c->k3_g2 : 0u, ks,
                          c->k3_variant));
+    if (async) TRY_HIP(hipEventRecord(c->ev_k3, ks));
+    c->k3_async = async;
   } else {
     TRY_HIP(launch_finalize(c->d_batch, c->d_persist, out_cap, out_n_dev, ctr_dev, cfg->direction, s));
   }
@@ -490,13 +555,22 @@ int tcbee_parse_finish_device(tcbee_ctx* c, const uint32_t* id_map_dev, uint64_t
   TRY_HIP(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   CountArgs k = c->pend;
+  if (id_map_dev && !c->d_omap) TRY_HIP(dalloc(&c->d_omap, c->nslots));
+  hipStream_t ks = s;
+  if (c->pend_ids) {  // async: after everything queued on `s` (K2, the id map)
+    TRY_HIP(hipEventRecord(c->ev_fin, s));
+    TRY_HIP(hipStreamWaitEvent(c->pend_ids, c->ev_fin, 0));
+    ks = c->pend_ids;
+  }
   if (id_map_dev) {
-    if (!c->d_omap) TRY_HIP(dalloc(&c->d_omap, c->nslots));
-    TRY_HIP(launch_compose(c->tab.cmap, id_map_dev, map_len, c->d_batch, c->d_omap, c->nslots, s));
+    TRY_HIP(launch_compose(c->tab.cmap, id_map_dev, map_len, k.batch, c->d_omap, c->nslots, ks));
     k.omap = c->d_omap;
   }
   c->count_pending = false;
-  TRY_HIP(launch_count(k, c->pend_g1, c->pend_g1s, c->pend_g2, s, c->k3_variant));
+  TRY_HIP(launch_count(k, c->pend_g1, c->pend_g1s, c->pend_g2, ks, c->k3_variant));
+  if (c->pend_ids) TRY_HIP(hipEventRecord(c->ev_k3, ks));
+  c->k3_async = c->pend_ids != nullptr;
+  c->pend_ids = nullptr;
   return TCBEE_OK;
 }
 
@@ -519,7 +593,6 @@ int tcbee_flow_first_frames_device(tcbee_ctx* c, uint64_t* out_first_frame_dev, 
   g.frame_gidx = frame_gidx_dev;
   g.n_frames = n_frames;
   g.out_cap = rec_frame_dev ? rec_frame_cap : ~0ull;
-  g.k3_pending = c->count_pending;
   TRY_HIP(launch_first_frames(g, s));
   return TCBEE_OK;
 }
@@ -595,6 +668,7 @@ int tcbee_parse_batch(tcbee_ctx* c, const tcbee_frames* in, const tcbee_cfg* cfg
 int tcbee_flow_count(tcbee_ctx* c, uint64_t* n) {
   if (!c || !n) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
+  TRY_HIP(k3_wait_host(c));
   if (int rc = apply_pending_reset(c, c->stream)) return rc;
   PersistState p{};
   TRY_HIP(hipMemcpyAsync(&p, c->d_persist, sizeof(p), hipMemcpyDeviceToHost, c->stream));
@@ -606,6 +680,7 @@ int tcbee_flow_count(tcbee_ctx* c, uint64_t* n) {
 int tcbee_flow_export(tcbee_ctx* c, tcbee_flow_entry* out, uint64_t cap, uint64_t* n) {
   if (!c || !n || (cap && !out)) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
+  TRY_HIP(k3_wait_host(c));
   if (int rc = apply_pending_reset(c, c->stream)) return rc;
   std::vector<uint64_t> meta, cnt;
   try {
@@ -642,6 +717,7 @@ int tcbee_flow_export_device(tcbee_ctx* c, tcbee_flow_entry* out_dev, uint64_t c
   if (!c || (cap && !out_dev)) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  TRY_HIP(k3_wait_stream(c, s));  // counters are K3's
   if (int rc = apply_pending_reset(c, s)) return rc;
   TRY_HIP(launch_export(c->tab, reinterpret_cast<uint64_t*>(out_dev), cap, c->d_persist, n_dev, s));
   return TCBEE_OK;
@@ -666,7 +742,7 @@ int tcbee_flow_export_global_device(tcbee_ctx* c, tcbee_flow_entry* out_dev, uin
   g.frame_gidx = frame_gidx_dev;
   g.n_frames = n_frames;
   g.out_cap = rec_frame_dev ? rec_frame_cap : ~0ull;
-  g.k3_pending = c->count_pending;
+  TRY_HIP(k3_wait_stream(c, s));  // counters are K3's
   TRY_HIP(launch_export_global(g, s));
   return TCBEE_OK;
 }
@@ -762,6 +838,7 @@ int tcbee_remap_ids_device(uint32_t* ids_dev, uint64_t n_max, const uint64_t* n_
 int tcbee_ctx_status(tcbee_ctx* c) {
   if (!c) return TCBEE_EINVAL;
   if (hipSetDevice(c->device) != hipSuccess) return TCBEE_EDEVICE;
+  if (k3_wait_host(c) != hipSuccess) return TCBEE_EDEVICE;
   PersistState p{};
   if (hipMemcpyAsync(&p, c->d_persist, sizeof(p), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
@@ -779,6 +856,7 @@ int tcbee_ctx_status(tcbee_ctx* c) {
 int tcbee_ctx_count_mode(tcbee_ctx* c, int* mode) {
   if (!c || !mode) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
+  TRY_HIP(k3_wait_host(c));
   PersistState p{};
   TRY_HIP(hipMemcpyAsync(&p, c->d_persist, sizeof(p), hipMemcpyDeviceToHost, c->stream));
   TRY_HIP(hipStreamSynchronize(c->stream));

@@ -95,6 +95,9 @@ struct RankArgs {
   uint32_t* bprefix;    // per scan block: exclusive popcount prefix
   uint64_t nwords;
   uint64_t nblocks;
+  bool update_persist;  // parse (not merge): advance rec_base / flow_count when
+                        // done and zero the new ids' counters, so the batch's K3
+                        // may run on another stream beside the next batch's K1
 };
 
 // Launchers (tcbee_kernels.hip). All asynchronous on `s`.
@@ -165,8 +168,6 @@ struct GlobalExportArgs {
   const uint64_t* frame_gidx;
   uint64_t n_frames;
   uint64_t out_cap;  // records of the batch that have a rec_frame entry
-  bool k3_pending;   // called between K2 and a deferred K3: the persistent record
-                     // base and flow count are not advanced yet
 };
 hipError_t launch_export_global(const GlobalExportArgs& g, hipStream_t s);
 // Merged table (first_seen = global frame index): out[id] = number of this

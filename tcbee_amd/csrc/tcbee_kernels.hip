@@ -851,8 +851,8 @@ __global__ void k_prep(PrepArgs p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) m[j] = 0;
       m[6] = ~0ull;
-      p.tab.cnt[2 * s] = 0;
-      p.tab.cnt[2 * s + 1] = 0;
+      // (the by-id counters are zeroed by K2 as ids are handed out: the previous
+      //  batch's K3 may still be adding to them on another stream)
     }
   }
 }
@@ -866,6 +866,18 @@ __global__ void k_prep(PrepArgs p) {
 //  - otherwise mark + scan + assign: the bitmap is scanned by 16 waves, each over
 //    a contiguous word range read 64 consecutive words at a time (coalesced).
 constexpr uint32_t kRankSortMax = 2048;
+
+// End of a single-block rank: the batch is classified — advance the context's
+// record base and flow count (K1 of the next batch reads them; K3 no longer does)
+__device__ __forceinline__ void rank_done(const RankArgs& r, uint32_t tid, uint64_t base,
+                                          uint64_t fbase, uint64_t n_new) {
+  if (!r.update_persist) return;
+  __syncthreads();  // every thread has read the old base / fbase
+  if (tid == 0) {
+    r.persist->rec_base = base + r.batch->n_acc;
+    r.persist->flow_count = fbase + n_new;
+  }
+}
 
 __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
   __shared__ uint32_t s_fs[kRankSortMax];
@@ -893,7 +905,9 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
       const uint64_t sl = r.new_list[j];
       r.tab.meta[8 * sl + 7] = fbase + rank + 1;
       r.tab.cmap[fbase + j] = (uint32_t)(fbase + rank);
+      if (r.update_persist) r.tab.cnt[2 * (fbase + rank)] = r.tab.cnt[2 * (fbase + rank) + 1] = 0;
     }
+    rank_done(r, tid, base, fbase, n_new);
     return;
   }
   uint64_t wmax = 0;
@@ -967,7 +981,9 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
     }
     r.tab.meta[8 * s + 7] = id + 1;
     r.tab.cmap[fbase + j] = (uint32_t)id;
+    if (r.update_persist) r.tab.cnt[2 * id] = r.tab.cnt[2 * id + 1] = 0;
   }
+  rank_done(r, tid, base, fbase, n_new);
 }
 
 __global__ __launch_bounds__(kBlock) void k_mark(RankArgs r) {
@@ -1079,8 +1095,15 @@ __global__ void k_assign(RankArgs r) {
     }
     r.tab.meta[8 * s + 7] = id + 1;
     r.tab.cmap[fbase + j] = (uint32_t)id;
+    if (r.update_persist) r.tab.cnt[2 * id] = r.tab.cnt[2 * id + 1] = 0;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) r.batch->flow_total = fbase + n_new;
+}
+
+// after the multi-kernel rank: advance the context's record base / flow count
+__global__ void k_rank_done(RankArgs r) {
+  r.persist->rec_base += r.batch->n_acc;
+  r.persist->flow_count = r.batch->flow_total;
 }
 
 // K3: per accepted frame, claim index -> dense id (written for records p <
@@ -1437,8 +1460,8 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
       c.ctr->handled += written;                // EVENTS_HANDLED, xdp.rs:214
       c.ctr->dropped += n_acc - written;        // EVENTS_DROPPED, xdp.rs:217
     }
-    c.persist_rw->rec_base += n_acc;
-    c.persist_rw->flow_count = nflows;
+    // (rec_base / flow_count were advanced by K2: this may run on another stream
+    //  beside the next batch's K1, which reads them)
   }
   {
     // the first-seen bitmap back to all-zero (the rank kernels are done with it)
@@ -1771,9 +1794,9 @@ __global__ void k_export(FlowTable t, uint64_t* out, uint64_t cap, const Persist
 __global__ void k_export_global(GlobalExportArgs g) {
   const uint64_t nslots = g.tab.mask + 1;
   const uint64_t nacc = g.batch->n_acc;
-  const uint64_t lo = g.k3_pending ? g.persist->rec_base : g.persist->rec_base - nacc;
+  const uint64_t lo = g.persist->rec_base - nacc;  // advanced by K2
   const uint64_t hi = lo + nacc;
-  const uint64_t nflows = g.k3_pending ? g.batch->flow_total : g.persist->flow_count;
+  const uint64_t nflows = g.persist->flow_count;
   const bool identity = g.rec_frame == nullptr;
   const bool bad_batch = identity && nacc != g.n_frames;
   bool bad = false;
@@ -1852,9 +1875,9 @@ __global__ void k_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t
 __global__ void k_first_frames(GlobalExportArgs g) {
   const uint64_t nslots = g.tab.mask + 1;
   const uint64_t nacc = g.batch->n_acc;
-  const uint64_t lo = g.k3_pending ? g.persist->rec_base : g.persist->rec_base - nacc;
+  const uint64_t lo = g.persist->rec_base - nacc;  // advanced by K2
   const uint64_t hi = lo + nacc;
-  const uint64_t nflows = g.k3_pending ? g.batch->flow_total : g.persist->flow_count;
+  const uint64_t nflows = g.persist->flow_count;
   const bool identity = g.rec_frame == nullptr;
   const bool bad_batch = identity && nacc != g.n_frames;
   bool bad = false;
@@ -2238,6 +2261,7 @@ hipError_t launch_rank(const RankArgs& r, hipStream_t s) {
                      0, s, r);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, r);
   hipLaunchKernelGGL(k_assign, dim3(1024), dim3(kBlock), 0, s, r);
+  if (r.update_persist) hipLaunchKernelGGL(k_rank_done, dim3(1), dim3(1), 0, s, r);
   return hipGetLastError();
 }
 

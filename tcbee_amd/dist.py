@@ -204,15 +204,17 @@ class FlowHashExchange:
 
     def step(self, arena, arena_len: int, offset, caplen, ts_ns, n: int, out_rec, out_cap: int,
              out_hash, out_id, out_n, counters, stream: int, filter_port: int = 0,
-             direction: int = 0, rec_frame=None) -> None:
+             direction: int = 0, rec_frame=None, ids_stream: int | None = None) -> None:
         """Parse this rank's shard with global flow ids (torch's current stream must be
         `stream`). rec_frame (u32[out_cap]): the record -> frame map, needed when the
         shard holds frames the hook rejects; without it every frame must be accepted
-        (checked on the device: the context's status then reports TCBEE_ESHARD)."""
+        (checked on the device: the context's status then reports TCBEE_ESHARD).
+        ids_stream: K3 (global ids, pkts/bytes, counters, out_n) runs there, beside
+        the next step's parse; order readers of those outputs after it."""
         self.local.parse_device(arena, arena_len, offset, caplen, ts_ns, n, out_rec, out_cap,
                                 out_hash, out_id, out_n, counters, filter_port=filter_port,
                                 direction=direction, stream=stream, out_frame=rec_frame,
-                                defer_ids=True)
+                                defer_ids=True, ids_stream=ids_stream)
         self.local.first_frames_device(self.first, self.cap, self.n, self.gidx, self.gidx.numel(),
                                        rec_frame=rec_frame, rec_frame_cap=out_cap, stream=stream)
         all_gather_flat(self.all_n, self.n, self.group)

@@ -133,21 +133,25 @@ class PacketParser:
                      out_rec, out_cap: int, out_hash=None, out_id=None, out_n=None,
                      counters=None, filter_port: int = 0,
                      direction: int = _lib.DIR_INGRESS, flows: bool = True,
-                     stream: int | None = None, out_frame=None, defer_ids: bool = False) -> None:
+                     stream: int | None = None, out_frame=None, defer_ids: bool = False,
+                     ids_stream: int | None = None) -> None:
         """Asynchronous parse of frames already in HBM (pointers or torch tensors).
 
         out_n: device u64[1]; counters: device u64[4] (accumulated); out_frame:
         device u32[out_cap], the batch-local frame index of each record; defer_ids:
-        stop before K3 (finish_device writes ids, pkts/bytes, counters, out_n)."""
+        stop before K3 (finish_device writes ids, pkts/bytes, counters, out_n);
+        ids_stream: run K3 there, beside the next batch's K1 (order readers of
+        out_id / out_n / counters after that stream)."""
         fr = _lib.Frames(_ptr(arena), arena_len, _ptr(offset), _ptr(caplen), _ptr(ts_ns), n)
         cfg = _lib.Cfg(filter_port, direction, 0, 0 if flows else _lib.F_NO_FLOWS)
-        if out_frame is None and not defer_ids:
+        if out_frame is None and not defer_ids and not ids_stream:
             _lib.check(_lib.lib().tcbee_parse_batch_device(
                 self._h, C.byref(fr), C.byref(cfg), _ptr(out_rec), C.c_uint64(out_cap),
                 _ptr(out_hash), _ptr(out_id), _ptr(out_n), _ptr(counters),
                 C.c_void_p(stream or 0)), "tcbee_parse_batch_device")
             return
-        ex = _lib.ParseEx(_ptr(out_frame), _lib.EX_DEFER_IDS if defer_ids else 0)
+        ex = _lib.ParseEx(_ptr(out_frame), (_lib.EX_DEFER_IDS if defer_ids else 0)
+                          | (_lib.EX_ASYNC_IDS if ids_stream else 0), 0, ids_stream or None)
         _lib.check(_lib.lib().tcbee_parse_batch_device_ex(
             self._h, C.byref(fr), C.byref(cfg), _ptr(out_rec), C.c_uint64(out_cap),
             _ptr(out_hash), _ptr(out_id), _ptr(out_n), _ptr(counters), C.byref(ex),

@@ -505,3 +505,58 @@ def test_k3_range_mode_large_batches(gpu, oracle, pool, n):
                                                  ctr["dropped"]]
         assert p.status() == 0
         assert p.count_mode() == (3 if len(table) <= 3 * 12288 else 1)
+
+
+@pytest.mark.parametrize("reset", [False, True])
+@pytest.mark.parametrize("flows", [300, 40_000])
+def test_async_ids_stream_batches(gpu, oracle, reset, flows):
+    """TCBEE_EX_ASYNC_IDS: each batch's K3 (ids, pkts/bytes, counters, out_n) runs on
+    a side stream while the next batch parses (two alternating slots inside the
+    context; the next K2 waits for it). Four back-to-back batches, flow ids carried
+    across them or the table reset before each (the bench's cold table); every
+    record, id, counter and the final table vs the oracle."""
+    import torch
+    from tracegen import mixed_trace
+    nb, per = 4, 150_000
+    tr = mixed_trace(nb * per, seed=flows + 3, n_flows=flows)
+    parts = [tr.slice(i * per, (i + 1) * per) for i in range(nb)]
+    side = torch.cuda.Stream()
+    main = torch.cuda.current_stream().cuda_stream
+    dev = []
+    for t in parts:
+        d = {"arena": torch.from_numpy(np.concatenate([t.arena, np.zeros(64, np.uint8)])).cuda(),
+             "off": torch.from_numpy(t.offset.view(np.int64)).cuda(),
+             "len": torch.from_numpy(t.caplen.view(np.int32)).cuda(),
+             "ts": torch.from_numpy(t.ts_ns.view(np.int64)).cuda(),
+             "rec": torch.empty(per * 74 + 64, dtype=torch.uint8, device="cuda"),
+             "id": torch.empty(per, dtype=torch.int32, device="cuda"),
+             "n": torch.zeros(1, dtype=torch.int64, device="cuda"),
+             "ctr": torch.zeros(4, dtype=torch.int64, device="cuda")}
+        dev.append(d)
+    torch.cuda.synchronize()
+    with tcbee_amd.PacketParser(max_frames=per, max_flows=4 * flows + 4096) as p:
+        for d, t in zip(dev, parts):
+            if reset:
+                p.reset_flows(stream=main, sync=False)
+            p.parse_device(d["arena"], len(t.arena), d["off"], d["len"], d["ts"], t.n, d["rec"],
+                           t.n, None, d["id"], d["n"], d["ctr"], stream=main,
+                           ids_stream=side.cuda_stream)
+        torch.cuda.synchronize()
+        ft = oracle.new_flowtab(1 << 17)
+        try:
+            for i, (d, t) in enumerate(zip(dev, parts)):
+                if reset:
+                    oracle.free_flowtab(ft)
+                    ft = oracle.new_flowtab(1 << 17)
+                base = 0 if reset else int(sum(int(x["n"].item()) for x in dev[:i]))
+                rec, fh, fi, ctr, _ = oracle.parse(t, ft=ft, record_base=base)
+                k = int(d["n"].item())
+                assert k == len(rec)
+                assert np.array_equal(d["rec"][:k * 74].cpu().numpy().reshape(-1, 74), rec)
+                assert np.array_equal(d["id"][:k].cpu().numpy().view(np.uint32), fi)
+                assert d["ctr"].cpu().numpy().tolist() == [ctr["ingress"], 0, ctr["handled"], 0]
+            table = oracle.flows(ft)
+        finally:
+            oracle.free_flowtab(ft)
+        assert np.array_equal(p.flows(), table)
+        assert p.status() == 0
