@@ -116,10 +116,11 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     # slots, so that step i's exchange (side stream) overlaps step i+1's parse
     overlap = multi and not fhx and os.environ.get("TCBEE_BENCH_OVERLAP", "1") != "0"
     nbuf = 2 if overlap else 1
-    # K3 (ids, pkts/bytes, counters) of step i on a side stream beside step i+1's K1
-    # (TCBEE_EX_ASYNC_IDS; not with the contiguous merge, whose export reads the
-    # counters on the main stream right after the parse)
-    ids_side = (torch.cuda.Stream() if os.environ.get("TCBEE_BENCH_ASYNC", "1") != "0"
+    # TCBEE_BENCH_ASYNC=1: K3 (ids, pkts/bytes, counters) of step i on a side stream
+    # beside step i+1's K1 (TCBEE_EX_ASYNC_IDS). Off by default: measured slower
+    # (config 3 4.52 -> 4.65 ms/step, config-4 share 7.39 -> 7.66): K3's 1024-thread,
+    # 144 KiB-LDS workgroups take whole CUs from the HBM-bound K1
+    ids_side = (torch.cuda.Stream() if os.environ.get("TCBEE_BENCH_ASYNC", "0") == "1"
                 and (not multi or fhx) else None)
     ids_stream = ids_side.cuda_stream if ids_side is not None else None
     slots = [{"rec": torch.empty(n * 74 + 64, dtype=torch.uint8, device="cuda"),

@@ -174,3 +174,28 @@ def test_gpu_rccl_world1_exchange(gpu, oracle, tmp_path, mode):
     assert np.array_equal(x["rec"], rec) and np.array_equal(x["gids"], fi)
     assert np.array_equal(x["merged"].view(FLOW_DTYPE), table)
     assert int(x["ctr"][0]) == ctr["ingress"] and int(x["status"][0]) == 0
+
+
+def test_gpu_world4_flowhash_exchange_real_trace(gpu, oracle, tmp_path):
+    """Four gloo ranks on device 0: the flow-hash exchange's binary searches over
+    three other ranks' first-frame arrays, a real mixed trace with FILTER_PORT."""
+    import torch.multiprocessing as mp
+
+    import dist_worker
+    from tracegen import mixed_trace
+    from tcbee_amd.parser import FLOW_DTYPE
+    n, flows, cap, world = 120_000, 3000, 4096, 4
+    mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path), "fhx_real",
+                                        flows, 5201), nprocs=world, join=True)
+    tr = mixed_trace(n, seed=404, n_flows=flows)
+    rec, fh, fi, ctr, table = oracle.parse(tr, filter_port=5201)
+    acc = oracle.accept_mask(tr, filter_port=5201)
+    recidx = np.cumsum(acc) - 1
+    res = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    assert np.array_equal(np.sort(np.concatenate([x["gidx"] for x in res])), np.arange(n))
+    for x in res:
+        g = x["gidx"]
+        ri = recidx[g[acc[g]]]
+        assert np.array_equal(x["rec"], rec[ri]) and np.array_equal(x["gids"], fi[ri])
+        assert np.array_equal(x["merged"].view(FLOW_DTYPE), table)
+        assert int(x["ctr"][0]) == ctr["ingress"] and int(x["status"][0]) == 0
