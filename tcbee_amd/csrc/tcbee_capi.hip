@@ -25,6 +25,7 @@ struct tcbee_ctx {
   int k3_variant = 0;           // TCBEE_K3ABL: timing-only K3 ablations / tilings (A/B)
   bool k3_range = false;        // K3 mode 3 available (part rows sized for it)
   int k1_variant = 0;           // TCBEE_K1V: K1 staging/occupancy A/B variants
+  uint32_t async_k3_blocks = 0; // TCBEE_ASYNC_K3_BLOCKS: K3 grid cap with async ids (A/B)
   uint32_t plain_walk = kPlainWalk;  // TCBEE_WALK: K1 plain probe walk length (A/B)
   uint32_t pack_bits = 0;            // K1->K3 scratch packing (0: two words per record)
 
@@ -245,6 +246,7 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   if (const char* e = std::getenv("TCBEE_TEST_K3_NOBUCKET")) c->k3_no_bucket = std::atoi(e);
   if (const char* e = std::getenv("TCBEE_K3ABL")) c->k3_variant = std::atoi(e);
   if (const char* e = std::getenv("TCBEE_K1V")) c->k1_variant = std::atoi(e);
+  if (const char* e = std::getenv("TCBEE_ASYNC_K3_BLOCKS")) c->async_k3_blocks = (uint32_t)std::atoi(e);
   if (const char* e = std::getenv("TCBEE_WALK")) c->plain_walk = (uint32_t)std::atoi(e);
   if (const char* e = std::getenv("TCBEE_FPL")) {
     const int v = std::atoi(e);
@@ -524,6 +526,13 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     uint64_t g1s = (in->n + 8191) / 8192;
     if (g1s > 2ull * c->n_cu) g1s = 2ull * c->n_cu;
     if (g1s == 0) g1s = 1;
+    if (async && c->async_k3_blocks) {
+      // A/B (TCBEE_ASYNC_K3_BLOCKS): a K3 beside the next K1 on fewer CUs
+      const uint64_t cap = c->async_k3_blocks;
+      if (g1 > cap && cap >= gmin) g1 = cap < 8 ? cap : cap / 8 * 8;
+      if (g1s > cap) g1s = cap;
+      k.g1 = (uint32_t)g1;
+    }
     if (defer) {
       c->pend = k;
       c->pend_g1 = (unsigned)g1;

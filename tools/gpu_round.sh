@@ -39,6 +39,9 @@ for s in "$@"; do
              step asyncab1 600 env TCBEE_BENCH_ASYNC=1 python bench.py --steps 20 --no-cpu --no-extra --sample-check && \
              step asyncab2 600 env TCBEE_BENCH_ASYNC=0 python bench.py --config4 --virtual-world 8 --steps 10 --no-cpu --no-extra --sample-check && \
              step asyncab3 600 env TCBEE_BENCH_ASYNC=1 python bench.py --config4 --virtual-world 8 --steps 10 --no-cpu --no-extra --sample-check ;;
+    asynccap) for g in 0 16 32 64; do step asynccap$g 600 env TCBEE_BENCH_ASYNC=1 TCBEE_ASYNC_K3_BLOCKS=$g python bench.py --steps 20 --no-cpu --no-extra --sample-check || exit 1; done; \
+              for g in 0 32 64; do step asynccapc4$g 600 env TCBEE_BENCH_ASYNC=1 TCBEE_ASYNC_K3_BLOCKS=$g python bench.py --config4 --virtual-world 8 --steps 10 --no-cpu --no-extra --sample-check || exit 1; done; \
+              step asynccapoff 600 env TCBEE_BENCH_ASYNC=0 python bench.py --steps 20 --no-cpu --no-extra --sample-check ;;
     capsweep) step capsweep 900 python tools/k1_sweep.py --fpl 2 --flows-only --workloads imix10k,imix125k,imix1M --frames 100000000 --rounds 2 --iters 3 --cap-mult 1,4,8,16 ;;
     smallprof) step smallprof 600 bash tools/small_prof.sh ;;
     xprof)  step xprof 600 env MASTER_ADDR=127.0.0.1 MASTER_PORT=29543 RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 TCBEE_BENCH_FORCE_MERGE=1 rocprofv3 --kernel-trace --stats -d gpurun_out/xprof -o run --output-format csv -- python bench.py --config4 --steps 5 --warmup 1 --no-cpu --no-extra --sample-check ;;
