@@ -170,6 +170,7 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
             with torch.cuda.stream(cs):  # the counters live on K3's stream
                 b["ctr"].zero_()
             p.reset_flows(stream=stream, sync=False)
+            fx.reset()
             fx.step(d_arena, alen, d_off, d_len, d_ts, n, b["rec"], n, b["hash"], b["id"],
                     b["n"], b["ctr"], stream, ids_stream=ids_stream)
             with torch.cuda.stream(cs):

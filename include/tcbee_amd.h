@@ -249,19 +249,28 @@ int tcbee_flow_export_global_device(tcbee_ctx* ctx, tcbee_flow_entry* out_dev, u
                                     uint64_t rec_frame_cap, void* stream);
 /* The flow-hash exchange: tables of the ranks are disjoint, so
  * global first-seen ids need only each flow's global first frame.
- * first_frames: out_first_frame_dev[local id] = global frame index of the flow's
- * first record (placed as tcbee_flow_export_global_device places it; same
- * TCBEE_ESHARD rule), n_dev[0] = the context's flows (capped at cap).
+ * Batches are WINDOWS of one global trace: window w covers the same global frame
+ * range on every rank (each rank parsing its shard's frames inside it), with the
+ * table kept across windows or reset before each.
+ * first_frames: for the flows first seen in the last batch (local ids [fbase,
+ * fbase + n_new)), out_first_frame_dev[id - fbase] = global frame index of the
+ * flow's first record (placed as tcbee_flow_export_global_device places it; same
+ * TCBEE_ESHARD rule, also if n_new > cap); n_dev[0] = n_new, n_dev[1] = fbase.
  * global_ids: from the all-gathered arrays (rank r's at all_first_frame_dev +
- * r*stride, its count at all_n_dev[r]) the local -> global id map of `rank`:
- * out_map_dev[l] = l + flows of other ranks whose first frame comes earlier. */
+ * r*stride, its {n_new, fbase} at all_n_dev[2r], [2r+1]) the local -> global ids
+ * of `rank`'s new flows: out_map_dev[fbase + l] = *gbase_in_dev + l + new flows of
+ * the other ranks first seen earlier (entries past map_cap are not written);
+ * *gbase_out_dev = *gbase_in_dev + every rank's n_new (global flows after this
+ * window; keep the two words as a ping-pong pair across windows, NULL in = 0).
+ * Earlier entries of out_map_dev (older flows) are left as they are. */
 int tcbee_flow_first_frames_device(tcbee_ctx* ctx, uint64_t* out_first_frame_dev, uint64_t cap,
                                    uint64_t* n_dev, const uint32_t* rec_frame_dev,
                                    const uint64_t* frame_gidx_dev, uint64_t n_frames,
                                    uint64_t rec_frame_cap, void* stream);
 int tcbee_global_ids_device(const uint64_t* all_first_frame_dev, const uint64_t* all_n_dev,
                             uint32_t world, uint32_t rank, uint64_t stride, uint32_t* out_map_dev,
-                            uint64_t map_cap, void* stream);
+                            uint64_t map_cap, const uint64_t* gbase_in_dev,
+                            uint64_t* gbase_out_dev, void* stream);
 /* After merging global-order exports, first_seen of the merged table is a global
  * FRAME index; the reference's is the global RECORD index (accepted frames
  * before it). This rank's share: out_counts_dev[id] = number of this rank's

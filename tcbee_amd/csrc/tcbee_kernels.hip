@@ -1869,15 +1869,19 @@ __global__ void k_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t
   }
 }
 
-// Flow-hash exchange (disjoint per-rank tables): per local id, the
-// global frame index of the flow's first record (same placement rules as
-// k_export_global), for the cheap global-id exchange.
+// Flow-hash exchange (disjoint per-rank tables): for the flows FIRST
+// SEEN IN THIS BATCH (local ids [fbase, fbase + n_new)), the global frame index of
+// each one's first record (placed as k_export_global places it) at out[id - fbase];
+// n_out = {n_new, fbase}. Batches are windows of one global trace (the same global
+// frame range on every rank), so the flows new in a window are exactly the union
+// of every rank's new flows, and older flows keep the ids they already have.
 __global__ void k_first_frames(GlobalExportArgs g) {
   const uint64_t nslots = g.tab.mask + 1;
   const uint64_t nacc = g.batch->n_acc;
   const uint64_t lo = g.persist->rec_base - nacc;  // advanced by K2
   const uint64_t hi = lo + nacc;
-  const uint64_t nflows = g.persist->flow_count;
+  const uint64_t nnew = g.batch->n_new;
+  const uint64_t fbase = g.persist->flow_count - nnew;
   const bool identity = g.rec_frame == nullptr;
   const bool bad_batch = identity && nacc != g.n_frames;
   bool bad = false;
@@ -1886,7 +1890,7 @@ __global__ void k_first_frames(GlobalExportArgs g) {
     const uint64_t* m = g.tab.meta + 8 * s;
     if (m[0] < 2 || m[7] == 0) continue;
     const uint64_t id = m[7] - 1;
-    if (id >= g.cap) continue;
+    if (id < fbase || id - fbase >= g.cap) continue;
     const uint64_t fs = m[6];
     uint64_t gfs = ~0ull;
     if (fs >= lo && fs < hi && fs - lo < g.out_cap && !bad_batch) {
@@ -1895,30 +1899,41 @@ __global__ void k_first_frames(GlobalExportArgs g) {
       if (fr < g.n_frames) gfs = g.frame_gidx[fr];
     }
     bad = bad || gfs == ~0ull;
-    g.out[id] = gfs;
+    g.out[id - fbase] = gfs;
   }
   if (__any(bad) && __lane_id() == 0) atomicOr(&g.persist->status, kStShard);
   if (g.n_out && blockIdx.x == 0 && threadIdx.x == 0) {
-    g.n_out[0] = nflows < g.cap ? nflows : g.cap;
-    if (bad_batch) atomicOr(&g.persist->status, kStShard);
+    g.n_out[0] = nnew < g.cap ? nnew : g.cap;
+    g.n_out[1] = fbase;
+    if (bad_batch || nnew > g.cap) atomicOr(&g.persist->status, kStShard);
   }
 }
 
-// gid[l] = l + (flows of the other ranks first seen before flow l of this rank):
-// each rank's first-frame array is ascending in its local ids (local ids are in
-// local first-seen order, a subsequence of the global trace), so a binary search
-// per other rank counts them; flows are disjoint across ranks, frames distinct.
+// gid[fbase_r + l] = gbase + l + (this window's new flows of the other ranks whose
+// first frame comes earlier): each rank's array is ascending (its new flows are in
+// local first-seen order, a subsequence of the global order; frames are distinct
+// across ranks), so one binary search per other rank counts them. gbase = global
+// flows of earlier windows; gbase_out = gbase + every rank's new flows.
 __global__ void k_global_ids(const uint64_t* allG, const uint64_t* alln, uint32_t world,
-                             uint32_t rank, uint64_t stride, uint32_t* gid, uint64_t cap) {
-  const uint64_t mine = alln[rank] < stride ? alln[rank] : stride;
-  for (uint64_t l = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; l < mine && l < cap;
+                             uint32_t rank, uint64_t stride, uint32_t* gid, uint64_t cap,
+                             const uint64_t* gbase_in, uint64_t* gbase_out) {
+  const uint64_t gbase = gbase_in ? *gbase_in : 0;
+  const uint64_t mine = alln[2 * rank] < stride ? alln[2 * rank] : stride;
+  const uint64_t fb = alln[2 * rank + 1];
+  if (gbase_out && blockIdx.x == 0 && threadIdx.x == 0) {
+    uint64_t tot = gbase;
+    for (uint32_t r = 0; r < world; ++r) tot += alln[2 * r];
+    *gbase_out = tot;
+  }
+  for (uint64_t l = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; l < mine;
        l += (uint64_t)gridDim.x * blockDim.x) {
+    if (fb + l >= cap) break;
     const uint64_t G = allG[(uint64_t)rank * stride + l];
-    uint64_t id = l;
+    uint64_t id = gbase + l;
     for (uint32_t r = 0; r < world; ++r) {
       if (r == rank) continue;
       const uint64_t* A = allG + (uint64_t)r * stride;
-      uint64_t lo = 0, len = alln[r] < stride ? alln[r] : stride;
+      uint64_t lo = 0, len = alln[2 * r] < stride ? alln[2 * r] : stride;
       while (len > 0) {
         const uint64_t half = len >> 1;
         if (A[lo + half] < G) {
@@ -1930,7 +1945,7 @@ __global__ void k_global_ids(const uint64_t* allG, const uint64_t* alln, uint32_
       }
       id += lo;
     }
-    gid[l] = (uint32_t)id;
+    gid[fb + l] = (uint32_t)id;
   }
 }
 
@@ -2346,10 +2361,9 @@ hipError_t launch_first_frames(const GlobalExportArgs& g, hipStream_t s) {
 
 hipError_t launch_global_ids(const uint64_t* allG, const uint64_t* alln, uint32_t world,
                              uint32_t rank, uint64_t stride, uint32_t* gid, uint64_t cap,
-                             hipStream_t s) {
-  const uint64_t n = stride < cap ? stride : cap;
-  hipLaunchKernelGGL(k_global_ids, dim3(grid_for(n)), dim3(kBlock), 0, s, allG, alln, world, rank,
-                     stride, gid, cap);
+                             const uint64_t* gbase_in, uint64_t* gbase_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_global_ids, dim3(grid_for(stride)), dim3(kBlock), 0, s, allG, alln, world,
+                     rank, stride, gid, cap, gbase_in, gbase_out);
   return hipGetLastError();
 }
 

@@ -183,51 +183,76 @@ class FlowHashExchange:
     the NIC-RSS step) give every rank a DISJOINT set of flows, so the global
     first-seen ids need only each flow's global first frame — no table merge.
     Per step, between K2 and K3 on the rank's stream:
-      tcbee_flow_first_frames_device (u64 per local id, ascending)
-      -> RCCL all-gather of those arrays (8 B x cap per rank) and of the flow counts
+      tcbee_flow_first_frames_device (u64 per flow new in this batch, ascending)
+      -> RCCL all-gather of those arrays (8 B x cap per rank) and of {n_new, fbase}
       -> tcbee_global_ids_device (binary searches in the other ranks' arrays)
       -> K3 (tcbee_parse_finish_device) writes the GLOBAL ids directly: no per-record
          remap pass, and per-flow counters stay with their one owner (nothing to
          reduce). The counters are all-reduced by the caller; the merged flow table
-         is assembled only on request (merged_flows)."""
+         is assembled only on request (merged_flows).
+    Steps are WINDOWS of one global trace (every rank's step k covers the same global
+    frame range, each rank parsing its shard's frames inside it): the flow table and
+    the local -> global id map (gmap, map_cap local flows) persist across windows, and
+    the global flow count rides a device ping-pong pair (gtot), so a stream of windows
+    gets the ids one parse of the whole trace would give. cap bounds the flows new in
+    one window on one rank; reset() goes with the context's reset_flows()."""
 
-    def __init__(self, local: "_parser.PacketParser", cap: int, gidx: torch.Tensor, group=None):
+    def __init__(self, local: "_parser.PacketParser", cap: int, gidx: torch.Tensor, group=None,
+                 map_cap: int | None = None):
         self.local, self.cap, self.gidx, self.group = local, cap, gidx, group
+        self.map_cap = map_cap or cap
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         dev = gidx.device
         self.first = torch.zeros(cap, dtype=torch.int64, device=dev)
-        self.n = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.n = torch.zeros(2, dtype=torch.int64, device=dev)
         self.all_first = torch.empty(self.world * cap, dtype=torch.int64, device=dev)
-        self.all_n = torch.empty(self.world, dtype=torch.int64, device=dev)
-        self.gmap = torch.empty(cap, dtype=torch.int32, device=dev)
+        self.all_n = torch.empty(2 * self.world, dtype=torch.int64, device=dev)
+        self.gmap = torch.empty(self.map_cap, dtype=torch.int32, device=dev)
+        self.gtot = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.windows = 0
+
+    def reset(self) -> None:
+        """Forget the global flow count (call with the context's reset_flows())."""
+        self.gtot.zero_()
+        self.windows = 0
 
     def step(self, arena, arena_len: int, offset, caplen, ts_ns, n: int, out_rec, out_cap: int,
              out_hash, out_id, out_n, counters, stream: int, filter_port: int = 0,
-             direction: int = 0, rec_frame=None, ids_stream: int | None = None) -> None:
-        """Parse this rank's shard with global flow ids (torch's current stream must be
-        `stream`). rec_frame (u32[out_cap]): the record -> frame map, needed when the
-        shard holds frames the hook rejects; without it every frame must be accepted
-        (checked on the device: the context's status then reports TCBEE_ESHARD).
-        ids_stream: K3 (global ids, pkts/bytes, counters, out_n) runs there, beside
-        the next step's parse; order readers of those outputs after it."""
+             direction: int = 0, rec_frame=None, ids_stream: int | None = None,
+             gidx: torch.Tensor | None = None) -> None:
+        """Parse this rank's frames of the next window with global flow ids (torch's
+        current stream must be `stream`). gidx: the window's local frame -> global
+        frame index (default: the one given at construction). rec_frame (u32[out_cap]):
+        the record -> frame map, needed when the shard holds frames the hook rejects;
+        without it every frame must be accepted (checked on the device: the context's
+        status then reports TCBEE_ESHARD). ids_stream: K3 (global ids, pkts/bytes,
+        counters, out_n) runs there, beside the next step's parse; order readers of
+        those outputs after it."""
+        gidx = self.gidx if gidx is None else gidx
         self.local.parse_device(arena, arena_len, offset, caplen, ts_ns, n, out_rec, out_cap,
                                 out_hash, out_id, out_n, counters, filter_port=filter_port,
                                 direction=direction, stream=stream, out_frame=rec_frame,
                                 defer_ids=True, ids_stream=ids_stream)
-        self.local.first_frames_device(self.first, self.cap, self.n, self.gidx, self.gidx.numel(),
+        self.local.first_frames_device(self.first, self.cap, self.n, gidx, gidx.numel(),
                                        rec_frame=rec_frame, rec_frame_cap=out_cap, stream=stream)
         all_gather_flat(self.all_n, self.n, self.group)
         all_gather_flat(self.all_first, self.first, self.group)
+        b = self.windows & 1
         _parser.global_ids_device(self.all_first, self.all_n, self.world, self.rank, self.cap,
-                                  self.gmap, self.cap, stream=stream)
-        self.local.finish_device(self.gmap, self.cap, stream=stream)
+                                  self.gmap, self.map_cap, gbase_in=self.gtot[b:b + 1],
+                                  gbase_out=self.gtot[1 - b:2 - b], stream=stream)
+        self.windows += 1
+        self.local.finish_device(self.gmap, self.map_cap, stream=stream)
 
     def merged_flows(self, merged: "_parser.PacketParser", n_dev, n_max: int,
                      max_total_records: int, rec_frame=None):
         """The global flow table (FLOW_DTYPE, global id order, first_seen = global
         record index) on every rank: the global-order export, all-gather and merge of
-        FlowMerge, run once on request (collective: every rank must call it)."""
+        FlowMerge, run once on request (collective: every rank must call it). Needs the
+        table to hold one window (reset() + reset_flows() before each step): a flow
+        first seen in an earlier window has no first record in the last batch's
+        record -> frame map (TCBEE_ESHARD)."""
         fm = FlowMerge(self.local, merged, self.cap, max_total_records, self.group)
         fm.gidx = self.gidx
         s = torch.cuda.current_stream().cuda_stream

@@ -157,6 +157,7 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode, n_flows=3000, filter_po
                 b = slots[0]
                 b["ctr"].zero_()
                 p.reset_flows(stream=s, sync=False)
+                fx.reset()
                 fx.step(arena, alen, off, ln, ts, m, b["rec"], m, b["hash"], b["id"], b["n"],
                         b["ctr"], s, filter_port=filter_port, rec_frame=b["frame"])
                 dist.all_reduce(b["ctr"])
@@ -195,5 +196,71 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode, n_flows=3000, filter_po
                  gids=b["id"][:k].cpu().numpy().view(np.uint32),
                  ctr=b["ctr"].cpu().numpy(), merged=merged.view(np.uint8),
                  status=np.array([status]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_gpu_windows(rank, world, port, n, n_flows, bounds, cap, map_cap, result_dir,
+                    filter_port=0):
+    """FlowHashExchange over a STREAM of windows: global frames [bounds[w],
+    bounds[w+1]) form window w; each rank parses its flow-hash shard's frames inside
+    it as one batch, keeping its flow table and id map (no reset between windows).
+    Saves the concatenated records / global ids / global frame indices, the summed
+    counters and the local flow table with each flow's global id."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_stream(torch.cuda.Stream())
+    import tcbee_amd
+    from tcbee_amd import host
+    from tcbee_amd.dist import FlowHashExchange
+    from tracegen import mixed_trace
+
+    tr = mixed_trace(n, seed=404, n_flows=n_flows)
+    mine = np.nonzero(host.flowhash_owner(tr, world) == rank)[0].astype(np.int64)
+    arena = torch.zeros(len(tr.arena) + 64, dtype=torch.uint8, device="cuda")
+    arena[:len(tr.arena)] = torch.from_numpy(tr.arena).cuda()
+    wmax = max(int(((mine >= a) & (mine < b)).sum()) for a, b in zip(bounds, bounds[1:]))
+    rec = torch.empty(max(wmax, 1) * 74 + 64, dtype=torch.uint8, device="cuda")
+    hsh = torch.empty(max(wmax, 1), dtype=torch.int32, device="cuda")
+    ids = torch.empty(max(wmax, 1), dtype=torch.int32, device="cuda")
+    frame = torch.empty(max(wmax, 1), dtype=torch.int32, device="cuda")
+    nrec = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctr = torch.zeros(4, dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    out_rec, out_ids, out_g, tot = [], [], [], np.zeros(4, np.int64)
+    with tcbee_amd.PacketParser(max_frames=max(wmax, 1), max_flows=map_cap) as p:
+        fx = None
+        for a, b in zip(bounds, bounds[1:]):
+            g = mine[(mine >= a) & (mine < b)]
+            sub = tr.select(g)
+            off = torch.from_numpy(sub.offset.view(np.int64)).cuda()
+            ln = torch.from_numpy(sub.caplen.view(np.int32)).cuda()
+            ts = torch.from_numpy(sub.ts_ns.view(np.int64)).cuda()
+            gidx = torch.from_numpy(g).cuda()
+            if fx is None:
+                fx = FlowHashExchange(p, cap, gidx, map_cap=map_cap)
+            ctr.zero_()
+            fx.step(arena, len(tr.arena), off, ln, ts, len(g), rec, len(g), hsh, ids, nrec, ctr,
+                    s, filter_port=filter_port, rec_frame=frame, gidx=gidx)
+            dist.all_reduce(ctr)
+            torch.cuda.synchronize()
+            k = int(nrec.item())
+            out_rec.append(rec[:k * 74].cpu().numpy().reshape(-1, 74))
+            out_ids.append(ids[:k].cpu().numpy().view(np.uint32))
+            out_g.append(g[frame[:k].cpu().numpy().astype(np.int64)])
+            tot += ctr.cpu().numpy()
+        status = p.status()
+        flows = p.flows()
+        gmap = fx.gmap[:len(flows)].cpu().numpy().view(np.uint32)
+        gtot = int(fx.gtot[fx.windows & 1].item())
+    np.savez(os.path.join(result_dir, f"rank{rank}.npz"), rec=np.concatenate(out_rec),
+             gids=np.concatenate(out_ids), gidx=np.concatenate(out_g), ctr=tot,
+             flows=flows.view(np.uint8), gmap=gmap, gtot=np.array([gtot]),
+             status=np.array([status]))
     dist.barrier()
     dist.destroy_process_group()

@@ -199,3 +199,40 @@ def test_gpu_world4_flowhash_exchange_real_trace(gpu, oracle, tmp_path):
         assert np.array_equal(x["rec"], rec[ri]) and np.array_equal(x["gids"], fi[ri])
         assert np.array_equal(x["merged"].view(FLOW_DTYPE), table)
         assert int(x["ctr"][0]) == ctr["ingress"] and int(x["status"][0]) == 0
+
+
+@pytest.mark.parametrize("filter_port", [0, 5201])
+def test_gpu_world2_flowhash_exchange_windows(gpu, oracle, tmp_path, filter_port):
+    """A stream of windows through the flow-hash exchange (the tables are NOT reset
+    between windows): flows keep their global ids across windows and new ones get
+    the ids one parse of the whole trace gives. Ragged windows, one holding a single
+    frame (so one rank parses an empty batch). Records, global ids, counters, and
+    each rank's table rows (pkts/bytes/tuple at their global ids) vs the oracle."""
+    import torch.multiprocessing as mp
+
+    import dist_worker
+    from tracegen import mixed_trace
+    from tcbee_amd.parser import FLOW_DTYPE
+    n, flows, world = 150_000, 4000, 2
+    bounds = [0, 3, 41_000, 41_001, 97_000, n]
+    mp.spawn(dist_worker.run_gpu_windows, args=(world, free_port(), n, flows, bounds, 4096,
+                                                8192, str(tmp_path), filter_port),
+             nprocs=world, join=True)
+    tr = mixed_trace(n, seed=404, n_flows=flows)
+    rec, fh, fi, ctr, table = oracle.parse(tr, filter_port=filter_port)
+    acc = oracle.accept_mask(tr, filter_port=filter_port)
+    recidx = np.cumsum(acc) - 1
+    res = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    seen = np.zeros(len(table), dtype=np.int64)
+    for x in res:
+        ri = recidx[x["gidx"]]
+        assert np.array_equal(x["rec"], rec[ri]) and np.array_equal(x["gids"], fi[ri])
+        assert int(x["ctr"][0]) == ctr["ingress"] and int(x["ctr"][2]) == ctr["handled"]
+        assert int(x["status"][0]) == 0 and int(x["gtot"][0]) == len(table)
+        loc = x["flows"].view(FLOW_DTYPE)
+        gm = x["gmap"].astype(np.int64)
+        assert np.array_equal(loc["tuple"], table["tuple"][gm])
+        assert np.array_equal(loc["pkts"], table["pkts"][gm])
+        assert np.array_equal(loc["bytes"], table["bytes"][gm])
+        seen[gm] += 1
+    assert (seen == 1).all()  # the ranks' tables partition the global one
