@@ -80,6 +80,7 @@ struct tcbee_ctx {
 
   // deferred K3 (TCBEE_EX_DEFER_IDS): launched by tcbee_parse_finish_device
   bool count_pending = false;
+  bool pend_empty = false;  // deferred batch had no K3 (empty / no flows): finish is a no-op
   CountArgs pend{};
   unsigned pend_g1 = 0, pend_g1s = 0, pend_g2 = 0;
   uint32_t* d_omap = nullptr;  // composed claim -> output id (allocated on first use)
@@ -554,6 +555,10 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     c->k3_async = async;
   } else {
     TRY_HIP(launch_finalize(c->d_batch, c->d_persist, out_cap, out_n_dev, ctr_dev, cfg->direction, s));
+    if (defer) {  // keep the parse -> finish pairing of a deferred batch
+      c->count_pending = true;
+      c->pend_empty = true;
+    }
   }
   return TCBEE_OK;
 }
@@ -561,6 +566,10 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
 int tcbee_parse_finish_device(tcbee_ctx* c, const uint32_t* id_map_dev, uint64_t map_len,
                               void* stream) {
   if (!c || !c->count_pending || (map_len && !id_map_dev)) return TCBEE_EINVAL;
+  if (c->pend_empty) {
+    c->count_pending = c->pend_empty = false;
+    return TCBEE_OK;
+  }
   TRY_HIP(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   CountArgs k = c->pend;
@@ -611,7 +620,7 @@ int tcbee_global_ids_device(const uint64_t* all_first_frame_dev, const uint64_t*
                             uint64_t map_cap, const uint64_t* gbase_in_dev,
                             uint64_t* gbase_out_dev, void* stream) {
   if (!all_first_frame_dev || !all_n_dev || world == 0 || rank >= world ||
-      (map_cap && !out_map_dev) || gbase_in_dev == gbase_out_dev)
+      (map_cap && !out_map_dev) || (gbase_in_dev && gbase_in_dev == gbase_out_dev))
     return TCBEE_EINVAL;
   if (!stride) return TCBEE_OK;
   TRY_HIP(launch_global_ids(all_first_frame_dev, all_n_dev, world, rank, stride, out_map_dev,
