@@ -88,7 +88,7 @@ def build_shard_trace(torch, n_global, world, rank, sizes, kind, n_flows, seed, 
 
 
 def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup, seed,
-               multi=None, full_check=False, flowhash=False, vworld=0):
+               multi=None, full_check=False, flowhash=False, vworld=0, warm=False):
     import tcbee_amd
     stream = torch.cuda.current_stream().cuda_stream
     # multi: the N>1 exchange runs (also at N=1 under TCBEE_BENCH_FORCE_MERGE=1, a
@@ -180,7 +180,8 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
             if om is not None:
                 om.acquire(k)
             b["ctr"].zero_()
-        p.reset_flows(stream=stream, sync=False)
+        if not warm:  # warm (N=1 extra leg): the table persists, a recorder's steady state
+            p.reset_flows(stream=stream, sync=False)
         p.parse_device(d_arena, alen, d_off, d_len, d_ts, n, b["rec"], n, b["hash"], b["id"],
                        b["n"], b["ctr"], stream=stream, ids_stream=ids_stream)
         if om is not None:
@@ -239,7 +240,8 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
                                         sizes, kind, n_flows, seed, nrec, global_ids=multi))
     elif rank == 0 and full_check and not multi:
         check.update(validate_full(torch, last["rec"], last["hash"], last["id"], n, sizes, kind,
-                                   n_flows, seed, nrec, flows))
+                                   n_flows, seed, nrec, flows,
+                                   table_mult=count[0] if warm else 1))
     elif rank == 0:
         check.update(validate_sample(torch, last["rec"], last["hash"], n, sizes, kind, n_flows,
                                      seed, first, nrec))
@@ -281,10 +283,11 @@ def validate_shard(torch, d_rec, d_hash, d_id, gidx, n, sizes, kind, n_flows, se
 
 
 def validate_full(torch, d_rec, d_hash, d_id, n, sizes, kind, n_flows, seed, nrec, gpu_flows,
-                  chunk=2_000_000):
+                  chunk=2_000_000, table_mult=1):
     """Every record, flow hash and flow id of the timed run vs the oracle streamed over
     the same trace in chunks (one flow table carried across them), and the whole
-    flow table (untimed; config 3 at N=1)."""
+    flow table (untimed; config 3 at N=1). table_mult: the table saw the trace that
+    many times (warm leg): same flows, ids and first_seen, pkts/bytes multiplied."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import tcbee_amd
     from oracle_py import Oracle
@@ -310,6 +313,10 @@ def validate_full(torch, d_rec, d_hash, d_id, n, sizes, kind, n_flows, seed, nre
         table = orc.flows(ft)
     finally:
         orc.free_flowtab(ft)
+    if table_mult != 1:
+        table = table.copy()
+        table["pkts"] *= np.uint64(table_mult)
+        table["bytes"] *= np.uint64(table_mult)
     table_ok = len(table) == len(gpu_flows) and np.array_equal(table, gpu_flows)
     out = {"full_bit_exact": bool(ok), "full_records": n, "flow_table_exact": bool(table_ok),
            "full_check_s": round(time.perf_counter() - t0, 1)}
@@ -628,6 +635,14 @@ def main():
             out["config3_zipf"] = {"mpkts": round(args.frames * args.steps / z_el / 1e6, 1),
                                    "ms_per_step": round(z_el / args.steps * 1e3, 4),
                                    "k1_ms": round(z_k1, 4), "zipf_s": 1.1, "check": z_chk}
+            # steady state of a recorder: the same frames with the table kept across
+            # steps (every flow known: K1 hits only, K2 ranks nothing new)
+            w_el, w_k1, w_n, w_chk, _ = run_device(torch, None, 0, 1, args.frames, args.sizes, 1,
+                                                args.flows, args.steps, args.warmup, args.seed,
+                                                full_check=not args.sample_check, warm=True)
+            out["config3_warm_table"] = {"mpkts": round(args.frames * args.steps / w_el / 1e6, 1),
+                                         "ms_per_step": round(w_el / args.steps * 1e3, 4),
+                                         "k1_ms": round(w_k1, 4), "check": w_chk}
             # one GPU's shard of config 4 (1B frames / 8 GPUs, 1M flows): every flow
             # appears in every contiguous shard, so each GPU's table holds all 1M
             c4_n, c4_steps = 125_000_000, 5

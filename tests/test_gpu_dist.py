@@ -236,3 +236,18 @@ def test_gpu_world2_flowhash_exchange_windows(gpu, oracle, tmp_path, filter_port
         assert np.array_equal(loc["bytes"], table["bytes"][gm])
         seen[gm] += 1
     assert (seen == 1).all()  # the ranks' tables partition the global one
+
+
+def test_gpu_world2_flowhash_exchange_window_over_cap(gpu, tmp_path):
+    """More new flows in one window than the exchange's per-rank capacity: every
+    write stays inside its buffer and the context reports TCBEE_ESHARD."""
+    import torch.multiprocessing as mp
+
+    import dist_worker
+    from tcbee_amd import _lib
+    n, flows, world = 20_000, 1000, 2
+    mp.spawn(dist_worker.run_gpu_windows, args=(world, free_port(), n, flows, [0, 5000, n], 64,
+                                                4096, str(tmp_path), 0),
+             nprocs=world, join=True)
+    for r in range(world):
+        assert int(np.load(tmp_path / f"rank{r}.npz")["status"][0]) == _lib.ESHARD
