@@ -257,7 +257,9 @@ int tcbee_flow_export_global_device(tcbee_ctx* ctx, tcbee_flow_entry* out_dev, u
  * flow's first record (placed as tcbee_flow_export_global_device places it; same
  * TCBEE_ESHARD rule, also if n_new > cap); n_dev[0] = n_new, n_dev[1] = fbase.
  * global_ids: from the all-gathered arrays (rank r's at all_first_frame_dev +
- * r*stride, its {n_new, fbase} at all_n_dev[2r], [2r+1]) the local -> global ids
+ * r*stride, its {n_new, fbase} at all_n_dev[r*n_stride], [r*n_stride+1]; n_stride
+ * 0 = 2, a separate array — or n_dev placed at out_first_frame_dev + cap and the
+ * two gathered as ONE array of stride cap + 2, n_stride = stride) the local -> global ids
  * of `rank`'s new flows: out_map_dev[fbase + l] = *gbase_in_dev + l + new flows of
  * the other ranks first seen earlier (entries past map_cap are not written);
  * *gbase_out_dev = *gbase_in_dev + every rank's n_new (global flows after this
@@ -268,9 +270,9 @@ int tcbee_flow_first_frames_device(tcbee_ctx* ctx, uint64_t* out_first_frame_dev
                                    const uint64_t* frame_gidx_dev, uint64_t n_frames,
                                    uint64_t rec_frame_cap, void* stream);
 int tcbee_global_ids_device(const uint64_t* all_first_frame_dev, const uint64_t* all_n_dev,
-                            uint32_t world, uint32_t rank, uint64_t stride, uint32_t* out_map_dev,
-                            uint64_t map_cap, const uint64_t* gbase_in_dev,
-                            uint64_t* gbase_out_dev, void* stream);
+                            uint64_t n_stride, uint32_t world, uint32_t rank, uint64_t stride,
+                            uint32_t* out_map_dev, uint64_t map_cap,
+                            const uint64_t* gbase_in_dev, uint64_t* gbase_out_dev, void* stream);
 /* After merging global-order exports, first_seen of the merged table is a global
  * FRAME index; the reference's is the global RECORD index (accepted frames
  * before it). This rank's share: out_counts_dev[id] = number of this rank's

@@ -112,9 +112,9 @@ _SIGS = {
     "tcbee_flow_first_frames_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64,
                                                  C.c_void_p, C.c_void_p, C.c_void_p,
                                                  C.c_uint64, C.c_uint64, C.c_void_p]),
-    "tcbee_global_ids_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
-                                          C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
-                                          C.c_void_p, C.c_void_p]),
+    "tcbee_global_ids_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
+                                          C.c_uint32, C.c_uint64, C.c_void_p, C.c_uint64,
+                                          C.c_void_p, C.c_void_p, C.c_void_p]),
     "tcbee_parse_batch": (C.c_int, [C.c_void_p, C.POINTER(Frames), C.POINTER(Cfg),
                                     C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                     C.POINTER(C.c_uint64), C.POINTER(Counters)]),

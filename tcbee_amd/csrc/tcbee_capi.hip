@@ -616,15 +616,17 @@ int tcbee_flow_first_frames_device(tcbee_ctx* c, uint64_t* out_first_frame_dev, 
 }
 
 int tcbee_global_ids_device(const uint64_t* all_first_frame_dev, const uint64_t* all_n_dev,
-                            uint32_t world, uint32_t rank, uint64_t stride, uint32_t* out_map_dev,
-                            uint64_t map_cap, const uint64_t* gbase_in_dev,
-                            uint64_t* gbase_out_dev, void* stream) {
-  if (!all_first_frame_dev || !all_n_dev || world == 0 || rank >= world ||
+                            uint64_t n_stride, uint32_t world, uint32_t rank, uint64_t stride,
+                            uint32_t* out_map_dev, uint64_t map_cap,
+                            const uint64_t* gbase_in_dev, uint64_t* gbase_out_dev, void* stream) {
+  if (n_stride == 0) n_stride = 2;
+  if (!all_first_frame_dev || !all_n_dev || world == 0 || rank >= world || n_stride < 2 ||
       (map_cap && !out_map_dev) || (gbase_in_dev && gbase_in_dev == gbase_out_dev))
     return TCBEE_EINVAL;
   if (!stride) return TCBEE_OK;
-  TRY_HIP(launch_global_ids(all_first_frame_dev, all_n_dev, world, rank, stride, out_map_dev,
-                            map_cap, gbase_in_dev, gbase_out_dev, (hipStream_t)stream));
+  TRY_HIP(launch_global_ids(all_first_frame_dev, all_n_dev, n_stride, world, rank, stride,
+                            out_map_dev, map_cap, gbase_in_dev, gbase_out_dev,
+                            (hipStream_t)stream));
   return TCBEE_OK;
 }
 

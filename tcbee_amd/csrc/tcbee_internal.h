@@ -181,9 +181,10 @@ hipError_t launch_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t
 // Flow-hash exchange: first frame per local id (GlobalExportArgs.out = u64[cap]);
 // global ids from the all-gathered first-frame arrays; output-id composition.
 hipError_t launch_first_frames(const GlobalExportArgs& g, hipStream_t s);
-hipError_t launch_global_ids(const uint64_t* allG, const uint64_t* alln, uint32_t world,
-                             uint32_t rank, uint64_t stride, uint32_t* gid, uint64_t cap,
-                             const uint64_t* gbase_in, uint64_t* gbase_out, hipStream_t s);
+hipError_t launch_global_ids(const uint64_t* allG, const uint64_t* alln, uint64_t nstride,
+                             uint32_t world, uint32_t rank, uint64_t stride, uint32_t* gid,
+                             uint64_t cap, const uint64_t* gbase_in, uint64_t* gbase_out,
+                             hipStream_t s);
 hipError_t launch_compose(const uint32_t* cmap, const uint32_t* id_map, uint64_t map_len,
                           const BatchState* b, uint32_t* omap, uint64_t max_flows, hipStream_t s);
 hipError_t launch_merge(const MergeArgs& g, const RankArgs& r, hipStream_t s);

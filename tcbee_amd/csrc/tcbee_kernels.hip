@@ -1914,15 +1914,15 @@ __global__ void k_first_frames(GlobalExportArgs g) {
 // local first-seen order, a subsequence of the global order; frames are distinct
 // across ranks), so one binary search per other rank counts them. gbase = global
 // flows of earlier windows; gbase_out = gbase + every rank's new flows.
-__global__ void k_global_ids(const uint64_t* allG, const uint64_t* alln, uint32_t world,
-                             uint32_t rank, uint64_t stride, uint32_t* gid, uint64_t cap,
-                             const uint64_t* gbase_in, uint64_t* gbase_out) {
+__global__ void k_global_ids(const uint64_t* allG, const uint64_t* alln, uint64_t nstride,
+                             uint32_t world, uint32_t rank, uint64_t stride, uint32_t* gid,
+                             uint64_t cap, const uint64_t* gbase_in, uint64_t* gbase_out) {
   const uint64_t gbase = gbase_in ? *gbase_in : 0;
-  const uint64_t mine = alln[2 * rank] < stride ? alln[2 * rank] : stride;
-  const uint64_t fb = alln[2 * rank + 1];
+  const uint64_t mine = alln[nstride * rank] < stride ? alln[nstride * rank] : stride;
+  const uint64_t fb = alln[nstride * rank + 1];
   if (gbase_out && blockIdx.x == 0 && threadIdx.x == 0) {
     uint64_t tot = gbase;
-    for (uint32_t r = 0; r < world; ++r) tot += alln[2 * r];
+    for (uint32_t r = 0; r < world; ++r) tot += alln[nstride * r];
     *gbase_out = tot;
   }
   for (uint64_t l = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; l < mine;
@@ -1933,7 +1933,7 @@ __global__ void k_global_ids(const uint64_t* allG, const uint64_t* alln, uint32_
     for (uint32_t r = 0; r < world; ++r) {
       if (r == rank) continue;
       const uint64_t* A = allG + (uint64_t)r * stride;
-      uint64_t lo = 0, len = alln[2 * r] < stride ? alln[2 * r] : stride;
+      uint64_t lo = 0, len = alln[nstride * r] < stride ? alln[nstride * r] : stride;
       while (len > 0) {
         const uint64_t half = len >> 1;
         if (A[lo + half] < G) {
@@ -2359,11 +2359,12 @@ hipError_t launch_first_frames(const GlobalExportArgs& g, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_global_ids(const uint64_t* allG, const uint64_t* alln, uint32_t world,
-                             uint32_t rank, uint64_t stride, uint32_t* gid, uint64_t cap,
-                             const uint64_t* gbase_in, uint64_t* gbase_out, hipStream_t s) {
-  hipLaunchKernelGGL(k_global_ids, dim3(grid_for(stride)), dim3(kBlock), 0, s, allG, alln, world,
-                     rank, stride, gid, cap, gbase_in, gbase_out);
+hipError_t launch_global_ids(const uint64_t* allG, const uint64_t* alln, uint64_t nstride,
+                             uint32_t world, uint32_t rank, uint64_t stride, uint32_t* gid,
+                             uint64_t cap, const uint64_t* gbase_in, uint64_t* gbase_out,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(k_global_ids, dim3(grid_for(stride)), dim3(kBlock), 0, s, allG, alln, nstride,
+                     world, rank, stride, gid, cap, gbase_in, gbase_out);
   return hipGetLastError();
 }
 

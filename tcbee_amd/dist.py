@@ -184,7 +184,8 @@ class FlowHashExchange:
     first-seen ids need only each flow's global first frame — no table merge.
     Per step, between K2 and K3 on the rank's stream:
       tcbee_flow_first_frames_device (u64 per flow new in this batch, ascending)
-      -> RCCL all-gather of those arrays (8 B x cap per rank) and of {n_new, fbase}
+      -> ONE RCCL all-gather of those arrays with {n_new, fbase} appended (8 B x
+         (cap + 2) per rank)
       -> tcbee_global_ids_device (binary searches in the other ranks' arrays)
       -> K3 (tcbee_parse_finish_device) writes the GLOBAL ids directly: no per-record
          remap pass, and per-flow counters stay with their one owner (nothing to
@@ -204,10 +205,11 @@ class FlowHashExchange:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         dev = gidx.device
-        self.first = torch.zeros(cap, dtype=torch.int64, device=dev)
-        self.n = torch.zeros(2, dtype=torch.int64, device=dev)
-        self.all_first = torch.empty(self.world * cap, dtype=torch.int64, device=dev)
-        self.all_n = torch.empty(2 * self.world, dtype=torch.int64, device=dev)
+        # one all-gather per window: rank r's new-flow first frames, then its
+        # {n_new, fbase}, at r * (cap + 2)
+        self.buf = torch.zeros(cap + 2, dtype=torch.int64, device=dev)
+        self.first, self.n = self.buf[:cap], self.buf[cap:]
+        self.all_buf = torch.empty(self.world * (cap + 2), dtype=torch.int64, device=dev)
         self.gmap = torch.empty(self.map_cap, dtype=torch.int32, device=dev)
         self.gtot = torch.zeros(2, dtype=torch.int64, device=dev)
         self.windows = 0
@@ -236,12 +238,12 @@ class FlowHashExchange:
                                 defer_ids=True, ids_stream=ids_stream)
         self.local.first_frames_device(self.first, self.cap, self.n, gidx, gidx.numel(),
                                        rec_frame=rec_frame, rec_frame_cap=out_cap, stream=stream)
-        all_gather_flat(self.all_n, self.n, self.group)
-        all_gather_flat(self.all_first, self.first, self.group)
+        all_gather_flat(self.all_buf, self.buf, self.group)
         b = self.windows & 1
-        _parser.global_ids_device(self.all_first, self.all_n, self.world, self.rank, self.cap,
-                                  self.gmap, self.map_cap, gbase_in=self.gtot[b:b + 1],
-                                  gbase_out=self.gtot[1 - b:2 - b], stream=stream)
+        _parser.global_ids_device(self.all_buf, self.all_buf[self.cap:], self.world, self.rank,
+                                  self.cap + 2, self.gmap, self.map_cap,
+                                  gbase_in=self.gtot[b:b + 1], gbase_out=self.gtot[1 - b:2 - b],
+                                  stream=stream, n_stride=self.cap + 2)
         self.windows += 1
         self.local.finish_device(self.gmap, self.map_cap, stream=stream)
 

@@ -316,15 +316,16 @@ def remap_ids_device(ids, n_max: int, n_dev, id_map, map_len: int,
 
 def global_ids_device(all_first, all_n, world: int, rank: int, stride: int, out_map,
                       map_cap: int, gbase_in=None, gbase_out=None,
-                      stream: int | None = None) -> None:
+                      stream: int | None = None, n_stride: int = 2) -> None:
     """Global ids of `rank`'s flows new in this window, from the all-gathered
-    first-frame arrays ({n_new, fbase} per rank in all_n); gbase_in/out: device u64
-    words holding the global flow count before / after the window."""
+    first-frame arrays ({n_new, fbase} of rank r at all_n[r * n_stride]); gbase_in/out:
+    device u64 words holding the global flow count before / after the window."""
     if stream is None:
         import torch
         stream = torch.cuda.current_stream().cuda_stream
     _lib.check(_lib.lib().tcbee_global_ids_device(
-        _ptr(all_first), _ptr(all_n), world, rank, C.c_uint64(stride), _ptr(out_map),
+        _ptr(all_first), _ptr(all_n), C.c_uint64(n_stride), world, rank, C.c_uint64(stride),
+        _ptr(out_map),
         C.c_uint64(map_cap), _ptr(gbase_in), _ptr(gbase_out), C.c_void_p(stream or 0)),
         "tcbee_global_ids_device")
 
