@@ -111,10 +111,18 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
                                                                seed, first, stream)
     # N>1, flow-hash shards: disjoint tables, the global-id exchange runs between K2
     # and K3 (FlowHashExchange; TCBEE_BENCH_EXCHANGE=merge: the general table merge)
-    fhx = multi and flowhash and os.environ.get("TCBEE_BENCH_EXCHANGE", "fhx") == "fhx"
+    exch = os.environ.get("TCBEE_BENCH_EXCHANGE", "auto")
+    fhx = multi and flowhash and exch in ("auto", "fhx")
+    # N>1 contiguous shards: each flow merged at its hash owner (OwnerExchange, between
+    # K2 and K3) instead of every rank merging every table (TCBEE_BENCH_EXCHANGE=merge:
+    # the all-gather merge, overlapped on a side stream). World-1 rehearsal, config 4
+    # contiguous (1M flows): 10.54 ms/step owner vs 11.00 merge (whose side stream
+    # slows the next K1 7.46 -> 8.78 ms); at N=8 an owner merges 1/8 of the entries
+    ownx = multi and not flowhash and exch in ("auto", "owner")
     # N>1 contiguous shards (every rank sees every flow): the table merge; two output
     # slots, so that step i's exchange (side stream) overlaps step i+1's parse
-    overlap = multi and not fhx and os.environ.get("TCBEE_BENCH_OVERLAP", "1") != "0"
+    overlap = (multi and not fhx and not ownx
+               and os.environ.get("TCBEE_BENCH_OVERLAP", "1") != "0")
     nbuf = 2 if overlap else 1
     # TCBEE_BENCH_ASYNC=1: K3 (ids, pkts/bytes, counters) of step i on a side stream
     # beside step i+1's K1 (TCBEE_EX_ASYNC_IDS). Off by default: measured slower
@@ -142,8 +150,17 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     xcap = max(int(1.25 * flows_here) + 4096, 1 << 12)
     p = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=n, max_arena=0,
                                max_flows=cap)
-    merged = om = fm = fx = None
-    if fhx:
+    merged = om = fm = fx = ox = None
+    if ownx:
+        from tcbee_amd.dist import OwnerExchange
+        merged = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=1024,
+                                        max_arena=0, max_flows=world * xcap)
+        ocap = int(1.25 * n_flows / world) + 4096  # flows one owner merges
+        owner_ctx = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=1024,
+                                           max_arena=0, max_flows=ocap)
+        ox = OwnerExchange(p, owner_ctx, seg_cap=int(1.25 * flows_here / world) + 4096,
+                           owner_cap=ocap, map_cap=xcap, max_total_records=world * n)
+    elif fhx:
         from tcbee_amd.dist import FlowHashExchange
         merged = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=1024,
                                         max_arena=0, max_flows=world * xcap)
@@ -165,6 +182,13 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
         k = count[0] % nbuf
         count[0] += 1
         b = slots[k]
+        if ox is not None:
+            b["ctr"].zero_()
+            p.reset_flows(stream=stream, sync=False)
+            ox.step(d_arena, alen, d_off, d_len, d_ts, n, b["rec"], n, b["hash"], b["id"],
+                    b["n"], b["ctr"], stream)
+            dist.all_reduce(b["ctr"])
+            return
         if fx is not None:
             cs = ids_side if ids_side is not None else torch.cuda.current_stream()
             with torch.cuda.stream(cs):  # the counters live on K3's stream
@@ -218,6 +242,8 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     if fx is not None:
         # the global table, assembled once after the timed steps (not part of a step)
         flows = fx.merged_flows(merged, last["n"], n, n_global)
+    elif ox is not None:
+        flows = ox.merged_flows(merged, last["n"], n)
     else:
         flows = (merged if merged is not None else p).flows()
     check = {"records": nrec, "flows": int(len(flows)), "status": status,
@@ -227,6 +253,10 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
         if fx is not None:
             check["exchange"] = ("flow-hash: first-frame all-gather (8 B x "
                                  f"{xcap} per rank) + global ids between K2 and K3")
+        if ox is not None:
+            check["exchange"] = (f"owner: all-to-all of {ox.seg_cap}-entry owner segments, "
+                                 "owner merge, first_seen all-gather, ids all-to-all back, "
+                                 "between K2 and K3")
         if om is not None:
             # side-stream span of one step's exchange (RCCL all-gather of the tables,
             # merge, id remap, counter all-reduce), overlapping the next parse
@@ -245,6 +275,8 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     elif rank == 0:
         check.update(validate_sample(torch, last["rec"], last["hash"], n, sizes, kind, n_flows,
                                      seed, first, nrec))
+    if ox is not None:
+        ox.owner.close()
     p.close()
     if merged is not None:
         merged.close()
@@ -549,7 +581,8 @@ def main():
                     help="N=1: check 2 x 200k records instead of every record + the table")
     args = ap.parse_args()
     if args.config4:
-        args.frames, args.flows, args.sizes, args.shard = 125_000_000, 1_000_000, "imix", "flowhash"
+        args.frames, args.flows, args.sizes = 125_000_000, 1_000_000, "imix"
+        args.shard = args.shard or "flowhash"
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))

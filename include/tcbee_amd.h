@@ -273,6 +273,40 @@ int tcbee_global_ids_device(const uint64_t* all_first_frame_dev, const uint64_t*
                             uint64_t n_stride, uint32_t world, uint32_t rank, uint64_t stride,
                             uint32_t* out_map_dev, uint64_t map_cap,
                             const uint64_t* gbase_in_dev, uint64_t* gbase_out_dev, void* stream);
+
+/* Owner exchange for CONTIGUOUS shards (every rank may hold every flow; SURVEY.md
+ * §8(e) option 2). Each flow is merged at one owner rank, owner =
+ * fold32(flow_hash64(key)) % world; per batch, between K2 and K3
+ * (TCBEE_EX_DEFER_IDS), all device-side and asynchronous on `stream`:
+ *  tcbee_owner_bucket_device: the context's flows into `world` segments of
+ *    seg_cap entries (segment o at ent_dev + o*seg_cap: key, pkts/bytes 0,
+ *    first_seen local), lid_dev = local id of each entry, meta_dev[0..world) =
+ *    entries per owner (the ones past seg_cap, and flows whose local id is not
+ *    below map_cap — the local -> global map's size — are dropped and the
+ *    context's status reports TCBEE_ESHARD), meta_dev[world] = the context's records;
+ *  -> all-gather of meta, all-to-all of the segments (rank r's segment o to o);
+ *  -> the owner merges what it received with tcbee_flow_merge_device (segment r
+ *    = rank r's entries, seg_meta {count, records of rank r}: first_seen rebased
+ *    to the global record stream) on a second context;
+ *  tcbee_flow_first_seen_device (on that context): out_dev[id] = first_seen of
+ *    flow id (ascending), n_dev = {flows, 0}: with tcbee_global_ids_device over
+ *    the all-gathered arrays, the owner's id -> global id map;
+ *  tcbee_owner_return_device: ret_dev[e] = gmap_dev[ids_dev[e]] for the valid
+ *    received entries (ids_dev: the merge's out_ids; seg_meta_dev as the merge's);
+ *  -> all-to-all back (each entry's global id returns to the place it was sent from);
+ *  tcbee_owner_apply_device: map_dev[lid_dev[e]] = back_dev[e] for the valid sent
+ *    entries: the local -> global id map for tcbee_parse_finish_device. */
+int tcbee_owner_bucket_device(tcbee_ctx* ctx, uint32_t world, uint64_t seg_cap, uint64_t map_cap,
+                              tcbee_flow_entry* ent_dev, uint32_t* lid_dev, uint64_t* meta_dev,
+                              void* stream);
+int tcbee_flow_first_seen_device(tcbee_ctx* ctx, uint64_t* out_dev, uint64_t cap, uint64_t* n_dev,
+                                 void* stream);
+int tcbee_owner_return_device(const uint32_t* ids_dev, const uint64_t* seg_meta_dev,
+                              uint32_t world, uint64_t seg_cap, const uint32_t* gmap_dev,
+                              uint64_t gmap_len, uint32_t* ret_dev, void* stream);
+int tcbee_owner_apply_device(const uint32_t* back_dev, const uint32_t* lid_dev,
+                             const uint64_t* meta_dev, uint32_t world, uint64_t seg_cap,
+                             uint32_t* map_dev, uint64_t map_cap, void* stream);
 /* After merging global-order exports, first_seen of the merged table is a global
  * FRAME index; the reference's is the global RECORD index (accepted frames
  * before it). This rank's share: out_counts_dev[id] = number of this rank's

@@ -615,6 +615,59 @@ int tcbee_flow_first_frames_device(tcbee_ctx* c, uint64_t* out_first_frame_dev, 
   return TCBEE_OK;
 }
 
+int tcbee_owner_bucket_device(tcbee_ctx* c, uint32_t world, uint64_t seg_cap, uint64_t map_cap,
+                              tcbee_flow_entry* ent_dev, uint32_t* lid_dev, uint64_t* meta_dev,
+                              void* stream) {
+  if (!c || world == 0 || world > kMaxOwners || !seg_cap || !ent_dev || !lid_dev || !meta_dev)
+    return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (int rc = apply_pending_reset(c, s)) return rc;
+  TRY_HIP(hipMemsetAsync(meta_dev, 0, (world + 1ull) * sizeof(uint64_t), s));
+  OwnerArgs a{};
+  a.tab = c->tab;
+  a.persist = c->d_persist;
+  a.world = world;
+  a.seg_cap = seg_cap;
+  a.map_cap = map_cap;
+  a.ent = reinterpret_cast<uint64_t*>(ent_dev);
+  a.lid = lid_dev;
+  a.meta = meta_dev;
+  a.status = &c->d_persist->status;
+  TRY_HIP(launch_owner_bucket(a, s));
+  return TCBEE_OK;
+}
+
+int tcbee_flow_first_seen_device(tcbee_ctx* c, uint64_t* out_dev, uint64_t cap, uint64_t* n_dev,
+                                 void* stream) {
+  if (!c || (cap && !out_dev)) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (int rc = apply_pending_reset(c, s)) return rc;
+  TRY_HIP(launch_first_seen(c->tab, c->d_persist, out_dev, cap, n_dev, s));
+  return TCBEE_OK;
+}
+
+int tcbee_owner_return_device(const uint32_t* ids_dev, const uint64_t* seg_meta_dev,
+                              uint32_t world, uint64_t seg_cap, const uint32_t* gmap_dev,
+                              uint64_t gmap_len, uint32_t* ret_dev, void* stream) {
+  if (!ids_dev || !seg_meta_dev || world == 0 || !seg_cap || !ret_dev || (gmap_len && !gmap_dev))
+    return TCBEE_EINVAL;
+  TRY_HIP(launch_owner_return(ids_dev, seg_meta_dev, world, seg_cap, gmap_dev, gmap_len, ret_dev,
+                              (hipStream_t)stream));
+  return TCBEE_OK;
+}
+
+int tcbee_owner_apply_device(const uint32_t* back_dev, const uint32_t* lid_dev,
+                             const uint64_t* meta_dev, uint32_t world, uint64_t seg_cap,
+                             uint32_t* map_dev, uint64_t map_cap, void* stream) {
+  if (!back_dev || !lid_dev || !meta_dev || world == 0 || !seg_cap || (map_cap && !map_dev))
+    return TCBEE_EINVAL;
+  TRY_HIP(launch_owner_apply(back_dev, lid_dev, meta_dev, world, seg_cap, map_dev, map_cap,
+                             (hipStream_t)stream));
+  return TCBEE_OK;
+}
+
 int tcbee_global_ids_device(const uint64_t* all_first_frame_dev, const uint64_t* all_n_dev,
                             uint64_t n_stride, uint32_t world, uint32_t rank, uint64_t stride,
                             uint32_t* out_map_dev, uint64_t map_cap,

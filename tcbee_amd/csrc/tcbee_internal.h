@@ -181,6 +181,34 @@ hipError_t launch_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t
 // Flow-hash exchange: first frame per local id (GlobalExportArgs.out = u64[cap]);
 // global ids from the all-gathered first-frame arrays; output-id composition.
 hipError_t launch_first_frames(const GlobalExportArgs& g, hipStream_t s);
+
+// Owner exchange for contiguous shards (SURVEY.md §8(e) option 2).
+constexpr uint32_t kMaxOwners = 64;
+constexpr int kOwnerItems = 4;  // slots per thread of k_owner_bucket
+struct OwnerArgs {
+  FlowTable tab;
+  const PersistState* persist;
+  uint32_t world;
+  uint64_t seg_cap;
+  uint64_t* ent;        // [world][seg_cap] tcbee_flow_entry (u64[8])
+  uint32_t* lid;        // [world][seg_cap] local id of each entry
+  uint64_t* meta;       // [world + 1]: entries per owner (zeroed first; may pass
+                        // seg_cap: the rest are dropped, TCBEE_ESHARD), records
+  uint64_t map_cap;     // local ids past it have no place in the id map: ESHARD
+  uint32_t* status;     // persist->status of the context (ESHARD on overflow)
+};
+hipError_t launch_owner_bucket(const OwnerArgs& a, hipStream_t s);
+// out[id] = first_seen of flow id (dense-id order: ascending), n_out = {flows, 0}
+hipError_t launch_first_seen(FlowTable t, const PersistState* p, uint64_t* out, uint64_t cap,
+                             uint64_t* n_out, hipStream_t s);
+// ret[r*seg_cap + j] = gmap[ids[r*seg_cap + j]] for j < min(seg_meta[2r], seg_cap)
+hipError_t launch_owner_return(const uint32_t* ids, const uint64_t* seg_meta, uint32_t world,
+                               uint64_t seg_cap, const uint32_t* gmap, uint64_t gmap_len,
+                               uint32_t* ret, hipStream_t s);
+// map[lid[o*seg_cap + j]] = back[o*seg_cap + j] for j < min(meta[o], seg_cap)
+hipError_t launch_owner_apply(const uint32_t* back, const uint32_t* lid, const uint64_t* meta,
+                              uint32_t world, uint64_t seg_cap, uint32_t* map, uint64_t map_cap,
+                              hipStream_t s);
 hipError_t launch_global_ids(const uint64_t* allG, const uint64_t* alln, uint64_t nstride,
                              uint32_t world, uint32_t rank, uint64_t stride, uint32_t* gid,
                              uint64_t cap, const uint64_t* gbase_in, uint64_t* gbase_out,

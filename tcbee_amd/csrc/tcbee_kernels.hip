@@ -1949,6 +1949,104 @@ __global__ void k_global_ids(const uint64_t* allG, const uint64_t* alln, uint64_
   }
 }
 
+// ---------------------------------------------------------------------------
+// Owner exchange (contiguous shards): every rank may hold every
+// flow, so each flow is merged at ONE owner rank, owner = fold32(flow_hash64(key))
+// % world (the NIC-RSS function of tcbee_flowhash_owner), instead of every rank
+// merging every table.
+// ---------------------------------------------------------------------------
+// The local table's flows bucketed by owner: per block, LDS counts per owner, one
+// device-scope reservation per (block, owner), then the entries at their places.
+__global__ __launch_bounds__(kBlock) void k_owner_bucket(OwnerArgs a) {
+  __shared__ uint32_t s_cnt[kMaxOwners];
+  __shared__ uint64_t s_base[kMaxOwners];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t nslots = a.tab.mask + 1;
+  if (tid < a.world) s_cnt[tid] = 0;
+  if (blockIdx.x == 0 && tid == 0) a.meta[a.world] = a.persist->rec_base;
+  __syncthreads();
+  uint32_t own[kOwnerItems], rank[kOwnerItems];
+  const uint64_t s0 = (uint64_t)blockIdx.x * kBlock * kOwnerItems + tid;
+#pragma unroll
+  for (int k = 0; k < kOwnerItems; ++k) {
+    own[k] = 0xFFFFFFFFu;
+    const uint64_t s = s0 + (uint64_t)k * kBlock;
+    if (s >= nslots) continue;
+    const uint64_t* m = a.tab.meta + 8 * s;
+    if (m[0] < 2 || m[7] == 0) continue;
+    own[k] = fold32(flow_hash64(m[1], m[2], m[3], m[4], m[5])) % a.world;
+    rank[k] = atomicAdd(&s_cnt[own[k]], 1u);
+  }
+  __syncthreads();
+  if (tid < a.world) {
+    const uint32_t c = s_cnt[tid];
+    s_base[tid] = c ? atomicAdd((unsigned long long*)&a.meta[tid], (unsigned long long)c) : 0ull;
+  }
+  __syncthreads();
+  bool over = false;
+#pragma unroll
+  for (int k = 0; k < kOwnerItems; ++k) {
+    if (own[k] == 0xFFFFFFFFu) continue;
+    const uint64_t pos = s_base[own[k]] + rank[k];
+    const uint64_t s = s0 + (uint64_t)k * kBlock;
+    const uint64_t* m = a.tab.meta + 8 * s;
+    if (pos >= a.seg_cap || m[7] - 1 >= a.map_cap) {
+      over = true;
+      continue;
+    }
+    const uint64_t e = (uint64_t)own[k] * a.seg_cap + pos;
+    uint64_t* out = a.ent + 8 * e;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) out[j] = m[1 + j];
+    out[5] = 0;  // pkts / bytes: K3 has not run (the ids come first)
+    out[6] = 0;
+    out[7] = m[6];  // first_seen, local to this rank's record stream
+    a.lid[e] = (uint32_t)(m[7] - 1);
+  }
+  if (__any(over) && __lane_id() == 0) atomicOr(a.status, kStShard);
+}
+
+__global__ void k_first_seen(FlowTable t, const PersistState* p, uint64_t* out, uint64_t cap,
+                             uint64_t* n_out) {
+  const uint64_t nslots = t.mask + 1;
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < nslots;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t* m = t.meta + 8 * s;
+    if (m[0] < 2 || m[7] == 0) continue;
+    const uint64_t id = m[7] - 1;
+    if (id < cap) out[id] = m[6];
+  }
+  if (n_out && blockIdx.x == 0 && threadIdx.x == 0) {
+    n_out[0] = p->flow_count < cap ? p->flow_count : cap;
+    n_out[1] = 0;
+  }
+}
+
+__global__ void k_owner_return(const uint32_t* ids, const uint64_t* seg_meta, uint32_t world,
+                               uint64_t seg_cap, const uint32_t* gmap, uint64_t gmap_len,
+                               uint32_t* ret) {
+  const uint64_t total = (uint64_t)world * seg_cap;
+  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
+       e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = e / seg_cap, j = e - r * seg_cap;
+    if (j >= seg_meta[2 * r]) continue;
+    const uint32_t id = ids[e];
+    ret[e] = id < gmap_len ? gmap[id] : 0xFFFFFFFFu;
+  }
+}
+
+__global__ void k_owner_apply(const uint32_t* back, const uint32_t* lid, const uint64_t* meta,
+                              uint32_t world, uint64_t seg_cap, uint32_t* map, uint64_t map_cap) {
+  const uint64_t total = (uint64_t)world * seg_cap;
+  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
+       e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t o = e / seg_cap, j = e - o * seg_cap;
+    if (j >= meta[o]) continue;
+    const uint32_t l = lid[e];
+    if (l < map_cap) map[l] = back[e];
+  }
+}
+
 // omap[claim] = id_map[cmap[claim]] for this batch's flows (output ids of K3)
 __global__ void k_compose(const uint32_t* cmap, const uint32_t* id_map, uint64_t map_len,
                           const BatchState* b, uint32_t* omap) {
@@ -2351,6 +2449,36 @@ hipError_t launch_records_before(FlowTable t, const uint32_t* rec_frame, const u
 
 hipError_t launch_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t cap, hipStream_t s) {
   hipLaunchKernelGGL(k_set_first_seen, dim3(grid_for(t.mask + 1)), dim3(kBlock), 0, s, t, fs_by_id, cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_owner_bucket(const OwnerArgs& a, hipStream_t s) {
+  const uint64_t per = (uint64_t)kBlock * kOwnerItems;
+  const uint64_t nb = (a.tab.mask + 1 + per - 1) / per;
+  hipLaunchKernelGGL(k_owner_bucket, dim3((unsigned)nb), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_first_seen(FlowTable t, const PersistState* p, uint64_t* out, uint64_t cap,
+                             uint64_t* n_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_first_seen, dim3(grid_for(t.mask + 1)), dim3(kBlock), 0, s, t, p, out, cap,
+                     n_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_owner_return(const uint32_t* ids, const uint64_t* seg_meta, uint32_t world,
+                               uint64_t seg_cap, const uint32_t* gmap, uint64_t gmap_len,
+                               uint32_t* ret, hipStream_t s) {
+  hipLaunchKernelGGL(k_owner_return, dim3(grid_for((uint64_t)world * seg_cap)), dim3(kBlock), 0, s,
+                     ids, seg_meta, world, seg_cap, gmap, gmap_len, ret);
+  return hipGetLastError();
+}
+
+hipError_t launch_owner_apply(const uint32_t* back, const uint32_t* lid, const uint64_t* meta,
+                              uint32_t world, uint64_t seg_cap, uint32_t* map, uint64_t map_cap,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(k_owner_apply, dim3(grid_for((uint64_t)world * seg_cap)), dim3(kBlock), 0, s,
+                     back, lid, meta, world, seg_cap, map, map_cap);
   return hipGetLastError();
 }
 

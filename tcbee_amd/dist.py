@@ -34,6 +34,18 @@ def all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
             p.copy_(t)
 
 
+def all_to_all_flat(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """Equal-split all-to-all: chunk r of inp goes to rank r, rank r's chunk for this
+    rank lands at chunk r of out (RCCL all_to_all_single; through host memory on
+    gloo, which exchanges CPU tensors)."""
+    if dist.get_backend(group) == "nccl":
+        dist.all_to_all_single(out, inp, group=group)
+    else:
+        tmp = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(tmp, inp.cpu(), group=group)
+        out.copy_(tmp)
+
+
 def gather_tables(entries: torch.Tensor, meta: torch.Tensor, group=None):
     """entries [cap, 8] int64 (this rank's exported table, padded to cap),
     meta [2] int64 {valid entries, records} -> (all_entries [world*cap, 8],
@@ -259,5 +271,88 @@ class FlowHashExchange:
         fm.gidx = self.gidx
         s = torch.cuda.current_stream().cuda_stream
         fm.step(None, n_dev, n_max, stream=s, rec_frame=rec_frame)
+        torch.cuda.synchronize()
+        return merged.flows()
+
+
+class OwnerExchange:
+    """Global flow ids for CONTIGUOUS shards (every rank may hold every flow) by flow
+    ownership — SURVEY.md §8(e) option 2 — instead of every rank merging every
+    table (FlowMerge): flow f is merged at rank fold32(flow_hash64(key)) % world.
+    Per step, between K2 and K3 on the rank's stream:
+      tcbee_owner_bucket_device (the local flows by owner: key + local first_seen)
+      -> all-gather of the per-owner counts and record counts
+      -> RCCL all-to-all of the owner segments (seg_cap entries of 64 B each)
+      -> the owner's merge of what it received (tcbee_flow_merge_device on `owner`:
+         first_seen rebased to the global record stream, min over ranks)
+      -> its flows' first_seen (ascending in its ids), one all-gather, global ids by
+         binary search (tcbee_global_ids_device, as the flow-hash exchange)
+      -> each received entry's global id back to its sender (all-to-all, 4 B)
+      -> the local -> global id map -> K3 writes global ids (no remap pass).
+    Traffic per rank: 64 B x its flows out and in, vs 64 B x every rank's flows in
+    with the all-gather merge. One batch per table (reset before each step), as
+    FlowMerge; merged_flows() assembles the global table on request."""
+
+    def __init__(self, local: "_parser.PacketParser", owner: "_parser.PacketParser",
+                 seg_cap: int, owner_cap: int, map_cap: int, max_total_records: int,
+                 group=None):
+        self.local, self.owner, self.group = local, owner, group
+        self.seg_cap, self.owner_cap, self.map_cap = seg_cap, owner_cap, map_cap
+        self.max_total = max_total_records
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        W = self.world
+        self.send = torch.zeros((W * seg_cap, ENTRY_WORDS), dtype=torch.int64, device=dev)
+        self.recv = torch.zeros_like(self.send)
+        self.lid = torch.zeros(W * seg_cap, dtype=torch.int32, device=dev)
+        self.meta = torch.zeros(W + 1, dtype=torch.int64, device=dev)
+        self.all_meta = torch.zeros(W * (W + 1), dtype=torch.int64, device=dev)
+        self.seg_meta = torch.zeros((W, 2), dtype=torch.int64, device=dev)
+        self.recv_ids = torch.zeros(W * seg_cap, dtype=torch.int32, device=dev)
+        self.fs = torch.zeros(owner_cap + 2, dtype=torch.int64, device=dev)
+        self.all_fs = torch.empty(W * (owner_cap + 2), dtype=torch.int64, device=dev)
+        self.gmap_o = torch.zeros(owner_cap, dtype=torch.int32, device=dev)
+        self.ret = torch.zeros(W * seg_cap, dtype=torch.int32, device=dev)
+        self.back = torch.zeros(W * seg_cap, dtype=torch.int32, device=dev)
+        self.gmap = torch.zeros(map_cap, dtype=torch.int32, device=dev)
+
+    def step(self, arena, arena_len: int, offset, caplen, ts_ns, n: int, out_rec, out_cap: int,
+             out_hash, out_id, out_n, counters, stream: int, filter_port: int = 0,
+             direction: int = 0) -> None:
+        """Parse this rank's contiguous shard with global flow ids (torch's current
+        stream must be `stream`); the caller all-reduces the counters."""
+        W, C = self.world, self.seg_cap
+        self.local.parse_device(arena, arena_len, offset, caplen, ts_ns, n, out_rec, out_cap,
+                                out_hash, out_id, out_n, counters, filter_port=filter_port,
+                                direction=direction, stream=stream, defer_ids=True)
+        self.local.owner_bucket_device(W, C, self.map_cap, self.send, self.lid, self.meta,
+                                       stream=stream)
+        all_gather_flat(self.all_meta, self.meta, self.group)
+        am = self.all_meta.view(W, W + 1)
+        # segment r of what this rank receives: rank r's entries for it, rank r's records
+        self.seg_meta[:, 0] = am[:, self.rank].clamp(max=C)
+        self.seg_meta[:, 1] = am[:, W]
+        all_to_all_flat(self.recv, self.send, self.group)
+        self.owner.merge_device(self.recv, W, C, self.seg_meta, self.max_total, self.recv_ids,
+                                stream=stream)
+        oc = self.owner_cap
+        self.owner.first_seen_device(self.fs[:oc], oc, self.fs[oc:], stream=stream)
+        all_gather_flat(self.all_fs, self.fs, self.group)
+        _parser.global_ids_device(self.all_fs, self.all_fs[oc:], W, self.rank, oc + 2,
+                                  self.gmap_o, oc, stream=stream, n_stride=oc + 2)
+        _parser.owner_return_device(self.recv_ids, self.seg_meta, W, C, self.gmap_o, oc,
+                                    self.ret, stream=stream)
+        all_to_all_flat(self.back, self.ret, self.group)
+        _parser.owner_apply_device(self.back, self.lid, self.meta, W, C, self.gmap,
+                                   self.map_cap, stream=stream)
+        self.local.finish_device(self.gmap, self.map_cap, stream=stream)
+
+    def merged_flows(self, merged: "_parser.PacketParser", n_dev, n_max: int):
+        """The global flow table on every rank (collective): the all-gather merge of
+        FlowMerge, once, on request."""
+        fm = FlowMerge(self.local, merged, self.map_cap, self.max_total, self.group)
+        s = torch.cuda.current_stream().cuda_stream
+        fm.step(None, n_dev, n_max, stream=s)
         torch.cuda.synchronize()
         return merged.flows()

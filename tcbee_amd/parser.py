@@ -225,8 +225,9 @@ class PacketParser:
     def first_frames_device(self, out, cap: int, n_dev, frame_gidx, n_frames: int,
                             rec_frame=None, rec_frame_cap: int = 0,
                             stream: int | None = None) -> None:
-        """out[local id] = global frame index of the flow's first record; n_dev[0] =
-        flows (the flow-hash exchange's per-rank input)."""
+        """For the flows first seen in the last batch (local ids fbase..): out[id -
+        fbase] = global frame index of the flow's first record; n_dev = {n_new,
+        fbase} (the flow-hash exchange's per-rank input)."""
         _lib.check(_lib.lib().tcbee_flow_first_frames_device(
             self._h, _ptr(out), C.c_uint64(cap), _ptr(n_dev), _ptr(rec_frame), _ptr(frame_gidx),
             C.c_uint64(n_frames), C.c_uint64(rec_frame_cap), C.c_void_p(stream or 0)),
@@ -245,6 +246,21 @@ class PacketParser:
         _lib.check(_lib.lib().tcbee_flow_set_first_seen_device(
             self._h, _ptr(fs_by_id), C.c_uint64(cap), C.c_void_p(stream or 0)),
             "tcbee_flow_set_first_seen_device")
+
+    def owner_bucket_device(self, world: int, seg_cap: int, map_cap: int, ent, lid, meta,
+                            stream: int | None = None) -> None:
+        """The table's flows into `world` owner segments of seg_cap entries (owner
+        exchange, contiguous shards); meta = {entries per owner..., records}."""
+        _lib.check(_lib.lib().tcbee_owner_bucket_device(
+            self._h, world, C.c_uint64(seg_cap), C.c_uint64(map_cap), _ptr(ent), _ptr(lid),
+            _ptr(meta),
+            C.c_void_p(stream or 0)), "tcbee_owner_bucket_device")
+
+    def first_seen_device(self, out, cap: int, n_dev, stream: int | None = None) -> None:
+        """out[id] = first_seen of flow id (ascending in id); n_dev = {flows, 0}."""
+        _lib.check(_lib.lib().tcbee_flow_first_seen_device(
+            self._h, _ptr(out), C.c_uint64(cap), _ptr(n_dev), C.c_void_p(stream or 0)),
+            "tcbee_flow_first_seen_device")
 
     def merge_device(self, entries, nseg: int, stride: int, seg_meta, max_total_records: int,
                      out_ids, stream: int | None = None) -> None:
@@ -333,3 +349,25 @@ def global_ids_device(all_first, all_n, world: int, rank: int, stride: int, out_
 def flow_hash64(key40: bytes) -> int:
     buf = (C.c_uint8 * 40).from_buffer_copy(bytes(key40))
     return int(_lib.lib().tcbee_flow_hash64(buf))
+
+
+def owner_return_device(ids, seg_meta, world: int, seg_cap: int, gmap, gmap_len: int, ret,
+                        stream: int | None = None) -> None:
+    """ret[e] = gmap[ids[e]] for the valid received entries of the owner exchange."""
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream().cuda_stream
+    _lib.check(_lib.lib().tcbee_owner_return_device(
+        _ptr(ids), _ptr(seg_meta), world, C.c_uint64(seg_cap), _ptr(gmap), C.c_uint64(gmap_len),
+        _ptr(ret), C.c_void_p(stream)), "tcbee_owner_return_device")
+
+
+def owner_apply_device(back, lid, meta, world: int, seg_cap: int, id_map, map_cap: int,
+                       stream: int | None = None) -> None:
+    """id_map[lid[e]] = back[e] for the valid sent entries: local -> global ids."""
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream().cuda_stream
+    _lib.check(_lib.lib().tcbee_owner_apply_device(
+        _ptr(back), _ptr(lid), _ptr(meta), world, C.c_uint64(seg_cap), _ptr(id_map),
+        C.c_uint64(map_cap), C.c_void_p(stream)), "tcbee_owner_apply_device")

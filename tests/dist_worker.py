@@ -40,6 +40,72 @@ def run(rank, world, port, n, cap, result_dir):
     dist.destroy_process_group()
 
 
+def run_owner(rank, world, port, n, cap, result_dir, filter_port=0):
+    """CPU mirror of tcbee_amd.dist.OwnerExchange over gloo (contiguous shards): the
+    oracle's shard table bucketed by owner (fold32 flow hash % world), the equal-split
+    all-to-all, the owner's merge (merge_ref), global ids from the all-gathered
+    owner first_seen arrays, and the ids sent back to the entries' senders."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from merge_ref import entries_to_table, merge, table_to_entries
+    from oracle_py import Oracle
+    from tracegen import mixed_trace
+
+    from tcbee_amd.dist import all_gather_flat, all_to_all_flat, shard_range
+
+    tr = mixed_trace(n, seed=404, n_flows=700)
+    lo, hi = shard_range(tr.n, rank, world)
+    rec, fh, fi, ctr, table = Oracle().parse(tr.slice(lo, hi), filter_port=filter_port)
+    # owner of each local flow: the fold32 hash of (any) one of its records
+    fhash = np.zeros(len(table), dtype=np.uint32)
+    fhash[fi] = fh
+    own = (fhash % world).astype(np.int64)
+    send = np.zeros((world, cap, 8), dtype=np.int64)
+    lid = np.zeros((world, cap), dtype=np.int64)
+    meta = np.zeros(world + 1, dtype=np.int64)
+    for o in range(world):
+        sel = np.nonzero(own == o)[0]
+        meta[o] = len(sel)
+        send[o] = table_to_entries(table[sel], cap)
+        lid[o, :len(sel)] = sel
+    meta[world] = len(rec)
+    all_meta = torch.zeros(world * (world + 1), dtype=torch.int64)
+    all_gather_flat(all_meta, torch.from_numpy(meta))
+    am = all_meta.numpy().reshape(world, world + 1)
+    recv = torch.zeros(world * cap, 8, dtype=torch.int64)
+    all_to_all_flat(recv, torch.from_numpy(send.reshape(-1, 8)))
+    recv = recv.numpy().reshape(world, cap, 8)
+    segs = [entries_to_table(recv[r], int(am[r, rank])) for r in range(world)]
+    owned, maps = merge(segs, [int(am[r, world]) for r in range(world)])
+    fs = np.zeros(cap + 1, dtype=np.int64)
+    fs[:len(owned)] = owned["first_seen"].astype(np.int64)
+    fs[cap] = len(owned)
+    all_fs = torch.zeros(world * (cap + 1), dtype=torch.int64)
+    all_gather_flat(all_fs, torch.from_numpy(fs))
+    af = all_fs.numpy().reshape(world, cap + 1)
+    gmap_o = np.arange(len(owned), dtype=np.int64)
+    for r in range(world):
+        if r != rank:
+            gmap_o += np.searchsorted(af[r, :af[r, cap]], fs[:len(owned)])
+    ret = np.zeros((world, cap), dtype=np.int64)
+    for r in range(world):
+        ret[r, :int(am[r, rank])] = gmap_o[maps[r]]
+    back = torch.zeros(world * cap, dtype=torch.int64)
+    all_to_all_flat(back, torch.from_numpy(ret.reshape(-1)))
+    back = back.numpy().reshape(world, cap)
+    gmap = np.zeros(len(table), dtype=np.int64)
+    for o in range(world):
+        gmap[lid[o, :meta[o]]] = back[o, :meta[o]]
+    gids = gmap[fi] if len(fi) else fi
+    np.savez(os.path.join(result_dir, f"rank{rank}.npz"), gids=gids, lo=lo, hi=hi)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def run_flowhash(rank, world, port, n, cap, result_dir, filter_port):
     """The flow-hash choreography on CPU (oracle tables, gloo collectives): host
     partition -> per-rank parse -> first_seen to global frame index through the
@@ -148,7 +214,23 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode, n_flows=3000, filter_po
     status = 0
     with tcbee_amd.PacketParser(max_frames=max(m, 1), max_flows=cap) as p, \
             tcbee_amd.PacketParser(max_frames=1024, max_flows=world * cap) as mg:
-        if fhx:
+        if mode == "owner":
+            from tcbee_amd.dist import OwnerExchange
+            # per-owner segments: a rank holds at most `cap` flows, an owner about
+            # 1/world of the global ones (generous here: tests cover small traces)
+            ox = OwnerExchange(p, mg, seg_cap=cap, owner_cap=cap, map_cap=cap,
+                               max_total_records=n)
+            for i in range(2):  # the second step re-uses every buffer of the first
+                b = slots[0]
+                b["ctr"].zero_()
+                p.reset_flows(stream=s, sync=False)
+                ox.step(arena, alen, off, ln, ts, m, b["rec"], m, b["hash"], b["id"], b["n"],
+                        b["ctr"], s, filter_port=filter_port)
+                dist.all_reduce(b["ctr"])
+            torch.cuda.synchronize()
+            status = p.status()
+            merged = ox.merged_flows(mg, b["n"], m)
+        elif fhx:
             from tcbee_amd.dist import FlowHashExchange
             fx = FlowHashExchange(p, cap, gidx if gidx is not None
                                   else torch.arange(m, dtype=torch.int64, device="cuda"))

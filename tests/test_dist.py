@@ -118,3 +118,21 @@ def test_flowhash_owner_matches_device_shards():
             + bytes([6, 0, 0, 0])
         h = orc_hash(key)
         assert own[i] == ((h ^ (h >> 32)) & 0xFFFFFFFF) % 4
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_owner_exchange_mirror(oracle, tmp_path, world):
+    """The owner exchange's algorithm (contiguous shards, flows merged at their hash
+    owner, ids by the owners' first_seen arrays, returned by all-to-all) on CPU
+    ranks over gloo: the global ids equal the unsharded oracle's."""
+    import torch.multiprocessing as mp
+
+    import dist_worker
+    from tracegen import mixed_trace
+    n, cap = 40_000, 2048
+    mp.spawn(dist_worker.run_owner, args=(world, free_port(), n, cap, str(tmp_path), 5201),
+             nprocs=world, join=True)
+    tr = mixed_trace(n, seed=404, n_flows=700)
+    fi = oracle.parse(tr, filter_port=5201)[2]
+    res = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    assert np.array_equal(np.concatenate([x["gids"] for x in res]), fi)

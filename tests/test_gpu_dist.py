@@ -20,7 +20,7 @@ def free_port():
     return p
 
 
-@pytest.mark.parametrize("mode", ["step", "overlap"])
+@pytest.mark.parametrize("mode", ["step", "overlap", "owner"])
 def test_gpu_world2_merge(gpu, oracle, tmp_path, mode):
     import torch.multiprocessing as mp
 
@@ -249,5 +249,43 @@ def test_gpu_world2_flowhash_exchange_window_over_cap(gpu, tmp_path):
     mp.spawn(dist_worker.run_gpu_windows, args=(world, free_port(), n, flows, [0, 5000, n], 64,
                                                 4096, str(tmp_path), 0),
              nprocs=world, join=True)
+    for r in range(world):
+        assert int(np.load(tmp_path / f"rank{r}.npz")["status"][0]) == _lib.ESHARD
+
+
+@pytest.mark.parametrize("world", [3, 4])
+@pytest.mark.parametrize("filter_port", [0, 5201])
+def test_gpu_owner_exchange_contiguous_real_trace(gpu, oracle, tmp_path, world, filter_port):
+    """The owner exchange over contiguous shards of a real mixed trace (rejected and
+    port-filtered frames, flows spanning every shard): records, global ids,
+    counters and the merged table vs the oracle over the whole trace."""
+    import torch.multiprocessing as mp
+
+    import dist_worker
+    from tracegen import mixed_trace
+    from tcbee_amd.parser import FLOW_DTYPE
+    n, flows, cap = 90_000, 3000, 8192
+    mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path), "owner",
+                                        flows, filter_port), nprocs=world, join=True)
+    tr = mixed_trace(n, seed=404, n_flows=flows)
+    rec, fh, fi, ctr, table = oracle.parse(tr, filter_port=filter_port)
+    res = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    assert np.array_equal(np.concatenate([x["rec"] for x in res]), rec)
+    assert np.array_equal(np.concatenate([x["gids"] for x in res]), fi)
+    for x in res:
+        assert np.array_equal(x["merged"].view(FLOW_DTYPE), table)
+        assert int(x["ctr"][0]) == ctr["ingress"] and int(x["status"][0]) == 0
+
+
+def test_gpu_owner_exchange_map_overflow_is_refused(gpu, tmp_path):
+    """A rank with more flows than the id map holds: the flows past it are not
+    exchanged and the local context reports TCBEE_ESHARD (no silent garbage ids)."""
+    import torch.multiprocessing as mp
+
+    import dist_worker
+    from tcbee_amd import _lib
+    n, flows, cap, world = 90_000, 3000, 4096, 2
+    mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path), "owner",
+                                        flows), nprocs=world, join=True)
     for r in range(world):
         assert int(np.load(tmp_path / f"rank{r}.npz")["status"][0]) == _lib.ESHARD
