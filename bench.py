@@ -220,6 +220,9 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     p.profile(True)
     if om is not None:
         om.spans.clear()
+    if fx is not None:
+        fx.timing = os.environ.get("TCBEE_BENCH_XTIME", "1") != "0"
+        fx.spans.clear()
     if multi:
         dist.barrier()
     torch.cuda.synchronize()
@@ -232,6 +235,7 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     t1 = time.perf_counter()
     k1_ms, k1_launches = p.profile_read()
     elapsed = t1 - t0
+    fx_ms = fx.exchange_ms() if fx is not None else None
     status = p.status()
 
     # validation (untimed): counts, flow table, and a bit-exact sample vs the oracle
@@ -252,7 +256,9 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
         check["ingress_global"] = int(last["ctr"][0].item())
         if fx is not None:
             check["exchange"] = ("flow-hash: first-frame all-gather (8 B x "
-                                 f"{xcap} per rank) + global ids between K2 and K3")
+                                 f"{xcap + 2} per rank) + global ids between K2 and K3")
+            # in-line span per step on the rank's stream (first frames .. global ids)
+            check["exchange_ms"] = round(fx_ms, 4) if fx_ms is not None else None
         if ox is not None:
             check["exchange"] = (f"owner: all-to-all of {ox.seg_cap}-entry owner segments, "
                                  "owner merge, first_seen all-gather, ids all-to-all back, "

@@ -225,11 +225,21 @@ class FlowHashExchange:
         self.gmap = torch.empty(self.map_cap, dtype=torch.int32, device=dev)
         self.gtot = torch.zeros(2, dtype=torch.int64, device=dev)
         self.windows = 0
+        self.spans = []  # (start, end) events of the exchange per step, when timing
+        self.timing = False
 
     def reset(self) -> None:
         """Forget the global flow count (call with the context's reset_flows())."""
         self.gtot.zero_()
         self.windows = 0
+
+    def exchange_ms(self) -> float | None:
+        """Mean span of the timed steps' exchanges (first frames -> global ids,
+        the all-gather included); synchronizes."""
+        if not self.spans:
+            return None
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in self.spans) / len(self.spans)
 
     def step(self, arena, arena_len: int, offset, caplen, ts_ns, n: int, out_rec, out_cap: int,
              out_hash, out_id, out_n, counters, stream: int, filter_port: int = 0,
@@ -248,6 +258,9 @@ class FlowHashExchange:
                                 out_hash, out_id, out_n, counters, filter_port=filter_port,
                                 direction=direction, stream=stream, out_frame=rec_frame,
                                 defer_ids=True, ids_stream=ids_stream)
+        if self.timing:  # the exchange's span on the stream: first frames .. global ids
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
         self.local.first_frames_device(self.first, self.cap, self.n, gidx, gidx.numel(),
                                        rec_frame=rec_frame, rec_frame_cap=out_cap, stream=stream)
         all_gather_flat(self.all_buf, self.buf, self.group)
@@ -256,6 +269,9 @@ class FlowHashExchange:
                                   self.cap + 2, self.gmap, self.map_cap,
                                   gbase_in=self.gtot[b:b + 1], gbase_out=self.gtot[1 - b:2 - b],
                                   stream=stream, n_stride=self.cap + 2)
+        if self.timing:
+            ev1.record()
+            self.spans.append((ev0, ev1))
         self.windows += 1
         self.local.finish_device(self.gmap, self.map_cap, stream=stream)
 
