@@ -295,7 +295,9 @@ int tcbee_global_ids_device(const uint64_t* all_first_frame_dev, const uint64_t*
  *    received entries (ids_dev: the merge's out_ids; seg_meta_dev as the merge's);
  *  -> all-to-all back (each entry's global id returns to the place it was sent from);
  *  tcbee_owner_apply_device: map_dev[lid_dev[e]] = back_dev[e] for the valid sent
- *    entries: the local -> global id map for tcbee_parse_finish_device. */
+ *    entries: the local -> global id map for tcbee_parse_finish_device.
+ * The context-free calls here and tcbee_global_ids_device read a NULL stream as
+ * HIP's null stream, as tcbee_remap_ids_device does: pass the caller's stream. */
 int tcbee_owner_bucket_device(tcbee_ctx* ctx, uint32_t world, uint64_t seg_cap, uint64_t map_cap,
                               tcbee_flow_entry* ent_dev, uint32_t* lid_dev, uint64_t* meta_dev,
                               void* stream);
