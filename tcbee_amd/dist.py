@@ -1,7 +1,14 @@
-"""The packet-record path over several GPUs: one process per GPU, each parsing a
-contiguous shard of one global frame stream (no frame exchange), then one RCCL
-exchange of the compact per-rank flow tables so that every rank holds the same
-merged table and global dense flow ids.
+"""The packet-record path over several GPUs: one process per GPU,
+every frame parsed once on one GPU (no frame exchange); only flow identities and
+counters cross GPUs, over RCCL:
+
+* FlowHashExchange — flow-hash shards (north_star's partition, NIC-RSS style):
+  disjoint tables, global first-seen ids from one all-gather of first frames;
+* OwnerExchange — contiguous shards: each flow merged at its hash owner
+  (all-to-all of owner segments, SURVEY.md §8(e) option 2);
+* FlowMerge / OverlappedMerge — the general all-gather table merge (any
+  partition; the merged table on request);
+* replay_pcap_sharded — a pcap replayed over the ranks into one .tcp file.
 
 The reference has no multi-node story; its per-CPU FLOWS maps
 (tcbee-ebpf/src/flow_tracker.rs:12-13) are the single-host analogue of the
@@ -9,6 +16,11 @@ per-rank tables merged here.
 """
 from __future__ import annotations
 
+import os
+import shutil
+import time
+
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -372,3 +384,63 @@ class OwnerExchange:
         fm.step(None, n_dev, n_max, stream=s)
         torch.cuda.synchronize()
         return merged.flows()
+
+
+def replay_pcap_sharded(pcap_path: str, out_prefix: str, direction: int = 0,
+                        filter_port: int = 0, db_path: str | None = None, metrics: bool = True,
+                        window: int = 80, chunk_frames: int = 1 << 20, threads: int = 8,
+                        group=None) -> dict:
+    """replay_pcap over the ranks of `group` (one process per GPU, collective): rank
+    r streams the contiguous frames shard_range(n, r, world) of the capture (a
+    zero-copy view of one mapping) through its own pinned pipeline into
+    <out_prefix><xdp|tc>.tcp.part<r>; rank 0 then appends the parts in rank order to
+    <out_prefix>xdp.tcp (or tc.tcp; BufferHandler append semantics: the bytes equal a
+    one-GPU replay), optionally runs the tcbee-process stage into db_path and writes
+    metrics.json with the all-reduced counters. Records only: no flow table is
+    needed for the files (tcbee-process assigns flows itself). Returns the global
+    counters, records and the slowest rank's seconds."""
+    from . import _lib, host
+    from .pipeline import Pipeline
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    name = "tc.tcp" if direction == _lib.DIR_EGRESS else "xdp.tcp"
+    part = f"{out_prefix}{name}.part{rank}"
+    if os.path.exists(part):
+        os.remove(part)
+    nccl = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device())
+    t0 = time.perf_counter()
+    with host.Pcap(pcap_path) as pc, Pipeline(device=torch.cuda.current_device(), window=window,
+                                              chunk_frames=chunk_frames,
+                                              threads=threads) as pipe:
+        tr = pc.trace()
+        lo, hi = shard_range(tr.n, rank, world)
+        sub = tr.select(np.arange(lo, hi, dtype=np.int64))
+        with host.TcpFile(part) as tf:
+            res = pipe.run(sub, filter_port=filter_port, direction=direction, flows=False,
+                           collect=False, sink=lambda rec, ids, first: tf.append(rec))
+        frames = tr.n
+    secs = time.perf_counter() - t0
+    keys = ("ingress", "egress", "handled", "dropped")
+    v = torch.tensor([res.counters[k] for k in keys] + [res.n], dtype=torch.int64,
+                     device=dev if nccl else "cpu")
+    dist.all_reduce(v, group=group)
+    t = torch.tensor([secs], dtype=torch.float64, device=dev if nccl else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    v, t = v.cpu().tolist(), float(t.item())
+    counters = dict(zip(keys, v[:4]))
+    out = {"frames": frames, "records": v[4], "counters": counters, "seconds": t,
+           "mpkts": frames / t / 1e6 if t > 0 else None, "ranks": world}
+    dist.barrier(group=group)
+    if rank == 0:
+        with open(out_prefix + name, "ab") as dst:
+            for r in range(world):
+                p = f"{out_prefix}{name}.part{r}"
+                with open(p, "rb") as src:
+                    shutil.copyfileobj(src, dst, 1 << 24)
+                os.remove(p)
+        if db_path:
+            out["sink"] = host.process_files(out_prefix, db_path)
+        if metrics:
+            host.write_metrics(out_prefix, counters)
+    dist.barrier(group=group)
+    return out

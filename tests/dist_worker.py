@@ -346,3 +346,22 @@ def run_gpu_windows(rank, world, port, n, n_flows, bounds, cap, map_cap, result_
              status=np.array([status]))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def run_replay(rank, world, port, pcap, prefix, db_path, filter_port, direction, result_dir):
+    """replay_pcap_sharded on `world` gloo ranks sharing device 0."""
+    import json
+
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tcbee_amd.dist import replay_pcap_sharded
+    out = replay_pcap_sharded(pcap, prefix, direction=direction, filter_port=filter_port,
+                              db_path=db_path, chunk_frames=4096, threads=2)
+    with open(os.path.join(result_dir, f"rank{rank}.json"), "w") as f:
+        json.dump({k: v for k, v in out.items() if k != "sink"}, f)
+    dist.destroy_process_group()

@@ -289,3 +289,38 @@ def test_gpu_owner_exchange_map_overflow_is_refused(gpu, tmp_path):
                                         flows), nprocs=world, join=True)
     for r in range(world):
         assert int(np.load(tmp_path / f"rank{r}.npz")["status"][0]) == _lib.ESHARD
+
+
+@pytest.mark.parametrize("world,filter_port,direction", [(2, 0, 0), (3, 5201, 1)])
+def test_gpu_replay_pcap_sharded(gpu, oracle, tmp_path, world, filter_port, direction):
+    """A pcap replayed over `world` ranks (contiguous shards, one pipeline each):
+    the one .tcp file, the counters in metrics.json and the tcbee-process database
+    equal the oracle path over the whole capture."""
+    import json
+    import os
+    import sys
+
+    import torch.multiprocessing as mp
+
+    import dist_worker
+    from tracegen import mixed_trace
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "oracle"))
+    import process_ref  # test infrastructure only
+    from tcbee_amd import host
+    t = mixed_trace(40_000, seed=77, n_flows=60)
+    pcap = str(tmp_path / "trace.pcap")
+    host.write_pcap(pcap, t)
+    prefix = str(tmp_path) + "/run_"
+    db = str(tmp_path / "gpu.sqlite")
+    mp.spawn(dist_worker.run_replay, args=(world, free_port(), pcap, prefix, db, filter_port,
+                                           direction, str(tmp_path)), nprocs=world, join=True)
+    rec, fh, fi, ctr, table = oracle.parse(t, filter_port=filter_port, direction=direction)
+    name = "tc.tcp" if direction else "xdp.tcp"
+    assert open(prefix + name, "rb").read() == rec.tobytes()
+    out = json.load(open(tmp_path / "rank0.json"))
+    assert out["records"] == len(rec) and out["counters"] == ctr and out["frames"] == t.n
+    m = json.load(open(prefix + "metrics.json"))
+    assert {k: m[k] for k in ("handled", "dropped", "ingress", "egress")} == ctr
+    process_ref.process_records(rec.tobytes(), str(tmp_path / "orc.sqlite"))
+    assert process_ref.dump_db(db) == process_ref.dump_db(str(tmp_path / "orc.sqlite"))
