@@ -404,7 +404,9 @@ int tcbee_gen_shard_index_device(uint64_t n_global, int world, int rank, int kin
  * window == 0: whole frames are shipped. window >= 80 (multiple of 16): only
  * the first min(caplen, window) bytes of each frame are shipped, with its
  * original caplen — the record path never reads past byte 74 of a frame, so
- * outputs are identical, and PCIe carries ~window+12 bytes per frame. */
+ * outputs are identical, and PCIe carries ~window+12 bytes per frame.
+ * window == 64: frame bytes [12, 76) (no record field reads the MAC addresses),
+ * one whole 64-B staging line per frame — the fastest gather. */
 typedef struct tcbee_pipe tcbee_pipe;
 typedef struct tcbee_pipe_cfg {
     uint64_t chunk_frames;  /* frames per chunk (0 = 1<<20)                     */

@@ -35,6 +35,7 @@ def check_same(res, orc, flows_gpu=None):
 @pytest.mark.parametrize("nt", ["1", "0"])
 @pytest.mark.parametrize("window,chunk,depth,threads", [
     (80, 4096, 3, 8), (80, 1000, 4, 1), (0, 4096, 3, 8), (96, 65536, 5, 3), (0, 777, 3, 2),
+    (64, 4096, 3, 8), (64, 1000, 4, 1),
 ])
 def test_pipeline_matches_oracle(gpu, oracle, window, chunk, depth, threads, nt, monkeypatch):
     """TCBEE_PIPE_NT=1 (default): the header-window gather copies whole windows with
@@ -50,11 +51,13 @@ def test_pipeline_matches_oracle(gpu, oracle, window, chunk, depth, threads, nt,
         assert st["frames"] == t.n and st["chunks"] >= t.n // chunk
 
 
+@pytest.mark.parametrize("window", [80, 64])
 @pytest.mark.parametrize("nt", ["1", "0"])
-def test_pipeline_windows_at_arena_end(gpu, oracle, nt, monkeypatch):
+def test_pipeline_windows_at_arena_end(gpu, oracle, nt, window, monkeypatch):
     """Runts and short frames packed back to back at the very end of the arena: their
-    80-B windows run past arena_len, so the gather falls back to a bounded copy
-    (zero fill past the arena) for exactly those frames."""
+    windows run past arena_len, so the gather falls back to a bounded copy (zero
+    fill past the arena) for exactly those frames; window 64 starts 12
+    bytes into each frame."""
     from tcbee_amd.trace import Trace
     monkeypatch.setenv("TCBEE_PIPE_NT", nt)
     t = mixed_trace(5000, seed=21, n_flows=40)
@@ -63,7 +66,7 @@ def test_pipeline_windows_at_arena_end(gpu, oracle, nt, monkeypatch):
     frames = [t.frame(i) for i in range(t.n)] + tail
     t2 = Trace.from_frames(frames)
     assert int(t2.offset[-1] + t2.caplen[-1]) == len(t2.arena)
-    with Pipeline(device=0, chunk_frames=1024, window=80, depth=3, threads=4,
+    with Pipeline(device=0, chunk_frames=1024, window=window, depth=3, threads=4,
                   max_flows=1 << 12) as p:
         check_same(p.run(t2), oracle.parse(t2), p.flows())
 

@@ -1,37 +1,53 @@
 #!/usr/bin/env python3
-"""E2E (host RAM -> GPU -> host RAM) pipeline rate of the tcbee_amd package under
-ROOT (argv[1]); header-window 80 and whole-frame staging, 20M IMIX frames."""
+"""A/B of the host-RAM end-to-end pipeline (tcbee_pipe) settings on one trace:
+header window bytes, staging depth, chunk size, gather threads."""
+import argparse
+import json
 import os
 import sys
 import time
 
 import numpy as np
 
-root = os.path.abspath(sys.argv[1] if len(sys.argv) > 1 else ".")
-sys.path.insert(0, root)
-import tcbee_amd  # noqa: E402
-from tcbee_amd.pipeline import Pipeline  # noqa: E402
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
-n = 20_000_000
-tr = tcbee_amd.synth_trace(n, sizes="imix", kind=1, n_flows=10_000)
-rec = np.empty((n, 74), np.uint8)
-ids = np.empty(n, np.uint32)
-pfs = [v for v in os.environ.get("PF_LIST", "").split(",") if v]
-nts = [v for v in os.environ.get("NT_LIST", "").split(",") if v]
-runs = ([(80, v, None) for v in pfs] + [(80, None, v) for v in nts]) or [(80, None, None),
-                                                                       (0, None, None)]
-for window, pf, nt in runs:
-    if pf is not None:
-        os.environ["TCBEE_PIPE_PF"] = pf
-    if nt is not None:
-        os.environ["TCBEE_PIPE_NT"] = nt
-    with Pipeline(device=0, chunk_frames=1 << 20, window=window, depth=4, threads=16,
-                  chunk_bytes=(1 << 29), max_flows=40_000) as p:
-        p.run(tr, out_rec=rec, out_id=ids)
-        ts = []
-        for _ in range(5):
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=20_000_000)
+    ap.add_argument("--variants", default="80:4:20:16,64:4:20:16,80:4:21:16,80:6:20:16,80:4:20:12")
+    ap.add_argument("--reps", type=int, default=9)
+    args = ap.parse_args()
+    import tcbee_amd
+    from tcbee_amd.pipeline import Pipeline
+    n = args.frames
+    tr = tcbee_amd.synth_trace(n, sizes="imix", kind=1, n_flows=10_000, seed=0x7CBEE)
+    rec = np.empty((n, 74), np.uint8)
+    ids = np.empty(n, np.uint32)
+    res = {}
+    pipes = {}
+    for v in args.variants.split(","):
+        w, depth, cbits, thr = (int(x) for x in v.split(":"))
+        pipes[v] = Pipeline(device=0, chunk_frames=1 << cbits, window=w, depth=depth, threads=thr,
+                            chunk_bytes=(1 << 29), max_flows=40_000)
+        pipes[v].run(tr, out_rec=rec, out_id=ids)  # warm-up
+    ts = {v: [] for v in pipes}
+    for _ in range(args.reps):  # interleaved: box drift hits every variant alike
+        for v, p in pipes.items():
             p.reset_flows()
             t0 = time.perf_counter()
-            p.run(tr, out_rec=rec, out_id=ids)
-            ts.append(time.perf_counter() - t0)
-    print(root, "window", window, "pf", pf, "nt", nt, "Mpkt/s", round(n / float(np.median(ts)) / 1e6, 1), flush=True)
+            r = p.run(tr, out_rec=rec, out_id=ids)
+            ts[v].append(time.perf_counter() - t0)
+            assert r.n == n
+    for v, p in pipes.items():
+        el = float(np.median(ts[v]))
+        res[v] = {"mpkts": round(n / el / 1e6, 1),
+                  "min_max": [round(n / max(ts[v]) / 1e6, 1), round(n / min(ts[v]) / 1e6, 1)]}
+        print(v, res[v], flush=True)
+        p.close()
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
