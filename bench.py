@@ -448,7 +448,8 @@ def cgroup_cpus():
 def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=5, threads=None):
     """End-to-end rates from host memory: frames in pageable host RAM -> records +
     flow ids back in pageable host RAM (H2D and D2H inside the timed region).
-      pipe_window80: tcbee_pipe, header-window staging (80 B/frame shipped)
+      pipe_window64: tcbee_pipe, header-window staging (frame bytes [12, 76): one
+                     64-B line per frame shipped; pipe_window80: bytes [0, 80))
       pipe_whole:    tcbee_pipe, whole frames shipped
       parse_batch:   one synchronous tcbee_parse_batch call (no overlap), 4M frames"""
     import numpy as np
@@ -460,7 +461,7 @@ def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=5, threads=None):
     rec = np.empty((n, 74), np.uint8)
     ids = np.empty(n, np.uint32)
     out = {"frames": n, "threads": threads, "arena_bytes": int(len(tr.arena))}
-    for name, window in (("pipe_window80", 80), ("pipe_whole", 0)):
+    for name, window in (("pipe_window64", 64), ("pipe_window80", 80), ("pipe_whole", 0)):
         with Pipeline(device=0, chunk_frames=1 << 20, window=window, depth=4, threads=threads,
                       chunk_bytes=(1 << 29), max_flows=max(4 * n_flows, 1 << 12)) as p:
             p.run(tr, out_rec=rec, out_id=ids)
@@ -471,7 +472,8 @@ def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=5, threads=None):
                 r = p.run(tr, out_rec=rec, out_id=ids)
                 ts.append(time.perf_counter() - t0)
             el = float(np.median(ts))
-        h2d = n * (window + 12) if window else int(len(tr.arena)) + 20 * n
+        h2d = n * (window + 12) + (64 if window == 64 else 0) if window else \
+            int(len(tr.arena)) + 20 * n
         out[name] = {"mpkts": round(n / el / 1e6, 1), "s": round(el, 4), "records": r.n,
                      "h2d_bytes": h2d, "h2d_GBs": round(h2d / el / 1e9, 1)}
     m = 4_000_000

@@ -388,7 +388,7 @@ class OwnerExchange:
 
 def replay_pcap_sharded(pcap_path: str, out_prefix: str, direction: int = 0,
                         filter_port: int = 0, db_path: str | None = None, metrics: bool = True,
-                        window: int = 80, chunk_frames: int = 1 << 20, threads: int = 8,
+                        window: int = 64, chunk_frames: int = 1 << 20, threads: int = 8,
                         group=None) -> dict:
     """replay_pcap over the ranks of `group` (one process per GPU, collective): rank
     r streams the contiguous frames shard_range(n, r, world) of the capture (a

@@ -28,7 +28,7 @@ class PipeResult:
 
 
 class Pipeline:
-    def __init__(self, device: int = 0, chunk_frames: int = 1 << 20, window: int = 80,
+    def __init__(self, device: int = 0, chunk_frames: int = 1 << 20, window: int = 64,
                  depth: int = 3, threads: int = 8, chunk_bytes: int = 0,
                  max_flows: int = 1 << 20):
         cfg = _lib.PipeCfg(chunk_frames, chunk_bytes, window, depth, threads, 0)
@@ -117,7 +117,7 @@ class Pipeline:
 
 def replay_pcap(pcap_path: str, out_prefix: str, direction: int = _lib.DIR_INGRESS,
                 filter_port: int = 0, db_path: str | None = None, metrics: bool = True,
-                device: int = 0, window: int = 80, chunk_frames: int = 1 << 20,
+                device: int = 0, window: int = 64, chunk_frames: int = 1 << 20,
                 threads: int = 8) -> dict:
     """pcap -> GPU record path -> <out_prefix>xdp.tcp|tc.tcp (appended), optionally
     the tcbee-process SQLite database at db_path (records pre-grouped by the GPU's
