@@ -173,7 +173,8 @@ struct tcbee_pipe {
   tcbee_ctx* ctx = nullptr;
   hipStream_t s_h2d = nullptr, s_comp = nullptr, s_d2h = nullptr;
   std::vector<Slot> slots;
-  Pool* pool = nullptr;
+  Pool* pool = nullptr;   // the gather (stage) threads, the main thread included
+  Pool* cpool = nullptr;  // the copy-out (consume) threads, the consumer thread included
   tcbee_pipe_stats st{};
   uint64_t prefetch = 48;  // header-window gather: frames ahead (TCBEE_PIPE_PF, 0 = off)
   int nt_copy = 1;         // header-window gather: fixed-size 16-B loads + streaming
@@ -202,6 +203,7 @@ void free_pipe(tcbee_pipe* p) {
   if (p->s_d2h) (void)hipStreamDestroy(p->s_d2h);
   if (p->ctx) tcbee_ctx_destroy(p->ctx);
   delete p->pool;
+  delete p->cpool;
   delete p;
 }
 
@@ -412,7 +414,14 @@ int tcbee_pipe_create(tcbee_pipe** out, int device, const tcbee_pipe_cfg* pc,
     return free_pipe(p), TCBEE_EDEVICE;
   try {
     p->slots.resize(c.depth);
-    p->pool = new Pool(c.threads);
+    // `threads` in all: a quarter copy records out while the rest gather
+    // (TCBEE_PIPE_CTHREADS: the copy-out share, A/B)
+    unsigned ct = c.threads >= 4 ? c.threads / 4 : 1;
+    if (const char* e = std::getenv("TCBEE_PIPE_CTHREADS")) ct = (unsigned)std::atoi(e);
+    if (ct < 1) ct = 1;
+    const unsigned gt = c.threads > ct ? c.threads - ct : 1;
+    p->pool = new Pool(gt);
+    p->cpool = new Pool(ct);
   } catch (...) {
     return free_pipe(p), TCBEE_ENOMEM;
   }
@@ -456,6 +465,9 @@ int tcbee_pipe_run(tcbee_pipe* p, const tcbee_frames* in, const tcbee_cfg* cfg,
   tcbee_counters sum{};
   int rc = TCBEE_OK;
 
+  // consume(c): counters, records (+ ids) into the caller's arrays, the sink call.
+  // It runs on a consumer thread with its own pool, in chunk order, overlapping
+  // the main thread's gather of later chunks (both are host-memory bound).
   auto consume = [&](Slot& s) -> int {
     TRY_HIP(hipEventSynchronize(s.ev_d2h));
     sum.ingress += s.h_meta[1];
@@ -468,7 +480,7 @@ int tcbee_pipe_run(tcbee_pipe* p, const tcbee_frames* in, const tcbee_cfg* cfg,
       const uint64_t k = n < out_cap - records ? n : out_cap - records;
       uint8_t* dst = out_rec74 + records * TCBEE_RECORD_BYTES;
       uint32_t* did = out_flow_id ? out_flow_id + records : nullptr;
-      p->pool->run([&](unsigned part, unsigned parts) {
+      p->cpool->run([&](unsigned part, unsigned parts) {
         const uint64_t a = k * part / parts, b = k * (part + 1) / parts;
         std::memcpy(dst + a * TCBEE_RECORD_BYTES, s.h_rec + a * TCBEE_RECORD_BYTES,
                     (b - a) * TCBEE_RECORD_BYTES);
@@ -483,33 +495,71 @@ int tcbee_pipe_run(tcbee_pipe* p, const tcbee_frames* in, const tcbee_cfg* cfg,
     }
     return TCBEE_OK;
   };
-
-  // Chunk c lives in slot c % D. Steady state at the top of an iteration:
-  // issued = i, fetched = i-1, consumed = i-2 — stage(i) overlaps H2D/parse of
-  // i-1 and the D2H of i-2 already in flight.
-  uint64_t lo = 0, issued = 0, fetched = 0, consumed = 0;
-  while (rc == TCBEE_OK && (lo < in->n || consumed < issued)) {
-    if (lo < in->n) {
-      while (rc == TCBEE_OK && consumed + D <= issued) {  // slot reuse
-        if (fetched <= consumed) rc = fetch(p, p->slots[fetched++ % D], flows);
-        if (rc == TCBEE_OK) rc = consume(p->slots[consumed++ % D]);
+  std::mutex cm;
+  std::condition_variable ccv;
+  uint64_t queued = 0, done = 0;  // chunks handed to / finished by the consumer
+  bool closing = false;
+  int crc = TCBEE_OK;
+  std::thread consumer([&] {
+    (void)hipSetDevice(p->device);
+    for (uint64_t j = 0;; ++j) {
+      {
+        std::unique_lock<std::mutex> lk(cm);
+        ccv.wait(lk, [&] { return j < queued || closing; });
+        if (j >= queued) return;  // closing, all consumed
       }
-      if (rc) break;
-      Slot& s = p->slots[issued % D];
-      s.lo = lo;
-      s.hi = chunk_end(p, in, lo);
-      stage(p, in, s);
-      if ((rc = enqueue(p, s, cfg))) break;
-      lo = s.hi;
-      ++issued;
-      ++chunks;
+      const int r = crc == TCBEE_OK ? consume(p->slots[j % D]) : crc;
+      {
+        std::lock_guard<std::mutex> g(cm);
+        if (r && crc == TCBEE_OK) crc = r;
+        done = j + 1;
+      }
+      ccv.notify_all();
     }
-    const bool tail = lo >= in->n;
-    if (fetched + 1 < issued || (tail && fetched < issued))
-      rc = fetch(p, p->slots[fetched++ % D], flows);
-    if (rc == TCBEE_OK && (consumed + 1 < fetched || (tail && consumed < fetched)))
-      rc = consume(p->slots[consumed++ % D]);
+  });
+  auto wait_done = [&](uint64_t need) -> int {
+    std::unique_lock<std::mutex> lk(cm);
+    ccv.wait(lk, [&] { return done >= need || crc != TCBEE_OK; });
+    return crc;
+  };
+  auto hand_over = [&](uint64_t j) {
+    {
+      std::lock_guard<std::mutex> g(cm);
+      queued = j + 1;
+    }
+    ccv.notify_all();
+  };
+
+  // Chunk c lives in slot c % D: it is staged once chunk c - D is consumed; chunk
+  // c - 1's records are fetched (D2H) after chunk c is enqueued, so stage(c)
+  // overlaps H2D/parse of c - 1 and the consumer's copy-out of earlier chunks.
+  uint64_t lo = 0, issued = 0, fetched = 0;
+  while (rc == TCBEE_OK && lo < in->n) {
+    if (issued >= D && (rc = wait_done(issued - D + 1))) break;
+    Slot& s = p->slots[issued % D];
+    s.lo = lo;
+    s.hi = chunk_end(p, in, lo);
+    stage(p, in, s);
+    if ((rc = enqueue(p, s, cfg))) break;
+    lo = s.hi;
+    ++issued;
+    ++chunks;
+    if (fetched + 1 < issued) {
+      if ((rc = fetch(p, p->slots[fetched % D], flows))) break;
+      hand_over(fetched++);
+    }
   }
+  while (rc == TCBEE_OK && fetched < issued) {
+    if ((rc = fetch(p, p->slots[fetched % D], flows))) break;
+    hand_over(fetched++);
+  }
+  {
+    std::lock_guard<std::mutex> g(cm);
+    closing = true;
+  }
+  ccv.notify_all();
+  consumer.join();
+  if (rc == TCBEE_OK) rc = crc;
   (void)hipStreamSynchronize(p->s_h2d);
   (void)hipStreamSynchronize(p->s_d2h);
   (void)tcbee_ctx_sync(p->ctx);

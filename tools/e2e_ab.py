@@ -28,7 +28,12 @@ def main():
     res = {}
     pipes = {}
     for v in args.variants.split(","):
-        w, depth, cbits, thr = (int(x) for x in v.split(":"))
+        f = [int(x) for x in v.split(":")]
+        w, depth, cbits, thr = f[:4]
+        if len(f) > 4:  # copy-out threads (TCBEE_PIPE_CTHREADS, read at create)
+            os.environ["TCBEE_PIPE_CTHREADS"] = str(f[4])
+        else:
+            os.environ.pop("TCBEE_PIPE_CTHREADS", None)
         pipes[v] = Pipeline(device=0, chunk_frames=1 << cbits, window=w, depth=depth, threads=thr,
                             chunk_bytes=(1 << 29), max_flows=40_000)
         pipes[v].run(tr, out_rec=rec, out_id=ids)  # warm-up
