@@ -118,7 +118,9 @@ void dfree(void* p) {
   if (p) (void)hipFree(p);
 }
 
-uint64_t tile_frames(int fpl) { return (uint64_t)kBlock * (uint64_t)fpl; }
+uint64_t tile_frames(int fpl, int k1v = 0) {
+  return (uint64_t)kBlock * (uint64_t)fpl * (k1v == 20 ? 2u : 1u);  // 20: 512-thread tiles
+}
 
 int ensure_host_path(tcbee_ctx* c) {
   if (c->d_arena) return TCBEE_OK;
@@ -420,7 +422,8 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
   uint32_t* const acc_flow = c->d_slot_scratch_s[c->slot];
   uint32_t* const acc_len = c->d_len_scratch_s[c->slot];
   const int fpl = c->fpl;
-  const uint64_t ntiles = (in->n + tile_frames(fpl) - 1) / tile_frames(fpl);
+  const uint64_t tf = tile_frames(fpl, flows && fpl == 2 ? c->k1_variant : 0);
+  const uint64_t ntiles = (in->n + tf - 1) / tf;
   const uint64_t nwords = flows && ntiles ? (in->n + 31) / 32 : 0;
   {
     PrepArgs pa{};

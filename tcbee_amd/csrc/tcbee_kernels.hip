@@ -396,7 +396,7 @@ __device__ __forceinline__ void lookback_publish(uint64_t* status, uint64_t tile
   st_agent(status + tile, (tile == 0 ? kFlagInc : kFlagAgg) | count);
 }
 
-template <int FPL>
+template <int TILE>
 __device__ uint32_t tile_accept_count(const ParseArgs& a, uint64_t tile);
 
 // Resolves this tile's exclusive prefix (one wave) and publishes its inclusive
@@ -404,7 +404,7 @@ __device__ uint32_t tile_accept_count(const ParseArgs& a, uint64_t tile);
 // whose word stays unpublished for kRecountSpins polls (not yet dispatched, or
 // slow) has its aggregate recounted from the input by this wave, so the walk
 // always terminates; results never depend on which block publishes first.
-template <int FPL>
+template <int TILE>
 __device__ uint64_t lookback_resolve(const ParseArgs& a, uint64_t tile, uint64_t count,
                                     bool withhold) {
   const uint32_t lane = __lane_id();
@@ -425,7 +425,7 @@ __device__ uint64_t lookback_resolve(const ParseArgs& a, uint64_t tile, uint64_t
       if (!need) break;
       if (++spins > kRecountSpins) {
         const uint32_t j = (uint32_t)__ffsll((unsigned long long)need) - 1;
-        const uint32_t cnt = tile_accept_count<FPL>(a, (uint64_t)(base - (int64_t)j));
+        const uint32_t cnt = tile_accept_count<TILE>(a, (uint64_t)(base - (int64_t)j));
         if (lane == j) v = kFlagAgg | cnt;
         spins = 0;
         continue;
@@ -475,9 +475,8 @@ __device__ __forceinline__ bool parse_frame(const uint8_t* __restrict__ arena, u
 
 // Accepted frames of one tile, recomputed from the input by one wave (the
 // look-back's fallback when a predecessor has not published).
-template <int FPL>
+template <int TILE>
 __device__ uint32_t tile_accept_count(const ParseArgs& a, uint64_t tile) {
-  constexpr int TILE = kBlock * FPL;
   const uint32_t lane = __lane_id();
   uint32_t cnt = 0;
   for (int k = 0; k < TILE / 64; ++k) {
@@ -545,14 +544,15 @@ __device__ __forceinline__ void wave_lds_sync() {
 // round (its records are contiguous in the output), 4.7 KB of LDS per wave.
 // OCC: minimum waves per SIMD requested from the register allocator (0: default)
 template <int FPL, bool FLOWS, int PROBE_AUX, int ABL = 0, int STAGE = 0, bool NT = false, int OCC = 0,
-          int HPOL = 0>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, OCC ? 8 : 8)))
+          int HPOL = 0, int BLK = kBlock>
+__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, OCC ? 8 : 8)))
 void k_parse(ParseArgs a) {
-  constexpr int TILE = kBlock * FPL;
+  constexpr int TILE = BLK * FPL;
+  constexpr int NW = BLK / 64;  // waves per tile
   constexpr int WBUF_DW = (64 * kRecBytes + 32) / 4;
-  constexpr int SREC_DW = STAGE ? 4 * WBUF_DW : (TILE * kRecBytes + 32) / 4;
+  constexpr int SREC_DW = STAGE ? NW * WBUF_DW : (TILE * kRecBytes + 32) / 4;
   __shared__ __attribute__((aligned(16))) uint32_t s_rec[SREC_DW];
-  __shared__ uint32_t s_wcnt[FPL][4];
+  __shared__ uint32_t s_wcnt[FPL][NW];
   __shared__ uint64_t s_excl;
 
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -571,7 +571,7 @@ void k_parse(ParseArgs a) {
   uint64_t offv[FPL], tsv[FPL];
 #pragma unroll
   for (int f = 0; f < FPL; ++f) {
-    const uint64_t i = i0 + (uint64_t)f * kBlock + tid;
+    const uint64_t i = i0 + (uint64_t)f * BLK + tid;
     acc[f] = false;
     slot[f] = 0xFFFFFFFFu;
     claim[f] = 0xFFFFFFFFu;
@@ -610,7 +610,7 @@ void k_parse(ParseArgs a) {
 #pragma unroll
   for (int f = 0; f < FPL; ++f) {
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const uint32_t c = s_wcnt[f][w];
       if ((uint32_t)w == wave) rank[f] += running;
       running += c;
@@ -710,7 +710,7 @@ void k_parse(ParseArgs a) {
           }
           if (slow)
             sl = flow_upsert(a.tab, K[f], h[f], a.batch, a.new_list, a.persist, fs, cl,
-                             kFsFlag | (i0 + (uint64_t)f * kBlock + tid));
+                             kFsFlag | (i0 + (uint64_t)f * BLK + tid));
         }
       }
       if (uni[f]) {
@@ -738,7 +738,7 @@ void k_parse(ParseArgs a) {
 
   if (wave == 0) {
     const uint64_t excl =
-        (ABL & 1) ? tile * (uint64_t)TILE : lookback_resolve<FPL>(a, tile, total, withhold);
+        (ABL & 1) ? tile * (uint64_t)TILE : lookback_resolve<TILE>(a, tile, total, withhold);
     if (lane == 0) s_excl = excl;
   }
   __syncthreads();
@@ -751,7 +751,7 @@ void k_parse(ParseArgs a) {
       const uint64_t wr_lo = excl < a.out_cap ? excl : a.out_cap;
       const uint64_t wr_hi = (excl + total) < a.out_cap ? (excl + total) : a.out_cap;
       if (wr_hi > wr_lo)
-        copy_out<NT>(a.out_rec, wr_lo * kRecBytes, wr_hi * kRecBytes, s_rec, tid, kBlock);
+        copy_out<NT>(a.out_rec, wr_lo * kRecBytes, wr_hi * kRecBytes, s_rec, tid, BLK);
     } else {
       uint32_t* wbuf = s_rec + wave * WBUF_DW;
 #pragma unroll
@@ -781,7 +781,7 @@ void k_parse(ParseArgs a) {
     if (acc[f] && !(ABL & 16)) {
       if (a.out_hash && p < a.out_cap) st_stream<NT>(a.out_hash + p, hsh[f]);
       // record -> frame map (flow-hash shards of traces with rejected frames)
-      if (a.out_frame && p < a.out_cap) st_stream<NT>(a.out_frame + p, (uint32_t)(i0 + (uint64_t)f * kBlock + tid));
+      if (a.out_frame && p < a.out_cap) st_stream<NT>(a.out_frame + p, (uint32_t)(i0 + (uint64_t)f * BLK + tid));
       if (FLOWS) {
         if (a.pack_bits) {
           // (claim, caplen) in one word; a caplen that does not fit saturates the
@@ -804,7 +804,7 @@ void k_parse(ParseArgs a) {
         const uint32_t leader = (uint32_t)__ffsll((unsigned long long)am) - 1;
         const uint32_t s0 = __shfl(slot[f], leader);
         const uint64_t gidx = rec_base + p;
-        const uint64_t frame_i = i0 + (uint64_t)f * kBlock + tid;
+        const uint64_t frame_i = i0 + (uint64_t)f * BLK + tid;
         if (__all(!mine || slot[f] == s0)) {
           // leader = lowest rank of the wave = its smallest accepted index
           if (lane == leader && fs_needs_min(fs_seen[f], frame_i, gidx))
@@ -2289,6 +2289,9 @@ static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s
       case 1: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 0>), grid, dim3(kBlock), 0, s, a); break;
       case 2: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 5>), grid, dim3(kBlock), 0, s, a); break;
       case 3: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 6>), grid, dim3(kBlock), 0, s, a); break;
+      // 512-thread tiles (1024 frames): half the tiles and look-back hops (A/B;
+      // the context sizes ntiles for it: k1_tile_blocks)
+      case 20: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 0, false, 0, 0, 512>), grid, dim3(512), 0, s, a); break;
 #define TCBEE_HPOL_CASE(P) \
       case 10 + P: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 0, false, 0, P>), grid, dim3(kBlock), 0, s, a); break;
       TCBEE_HPOL_CASE(1) TCBEE_HPOL_CASE(2) TCBEE_HPOL_CASE(3) TCBEE_HPOL_CASE(4) TCBEE_HPOL_CASE(5)
