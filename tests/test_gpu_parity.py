@@ -217,22 +217,25 @@ def test_arena_beyond_4GiB(parser, oracle):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("fpl", ["1", "2", "4"])
-def test_tile_shape_determinism(gpu, oracle, fpl, monkeypatch):
-    """Same trace, different frames-per-lane tilings -> identical outputs."""
+@pytest.mark.parametrize("fpl,k1v", [("1", "0"), ("2", "0"), ("4", "0"), ("2", "20")])
+def test_tile_shape_determinism(gpu, oracle, fpl, k1v, monkeypatch):
+    """Same trace, different frames-per-lane tilings (and 512-thread tiles,
+    TCBEE_K1V=20) -> identical outputs."""
     from tracegen import mixed_trace
     monkeypatch.setenv("TCBEE_FPL", fpl)
+    monkeypatch.setenv("TCBEE_K1V", k1v)
     tr = mixed_trace(150_000, seed=77, n_flows=2000)
     with tcbee_amd.PacketParser(max_frames=1 << 18, max_arena=1 << 26, max_flows=1 << 14) as p:
         assert_same(p.parse(tr), oracle.parse(tr), p.flows())
 
 
-@pytest.mark.parametrize("every", ["1", "3", "64"])
-def test_lookback_recount_fallback(gpu, oracle, every, monkeypatch):
+@pytest.mark.parametrize("every,k1v", [("1", "0"), ("3", "0"), ("64", "0"), ("3", "20")])
+def test_lookback_recount_fallback(gpu, oracle, every, k1v, monkeypatch):
     """Tiles that never publish force successors to recount them from the input:
     results stay exact (the look-back assumes no dispatch order)."""
     from tracegen import mixed_trace
     monkeypatch.setenv("TCBEE_TEST_WITHHOLD", every)
+    monkeypatch.setenv("TCBEE_K1V", k1v)
     tr = mixed_trace(20_000 if every == "1" else 60_000, seed=91, n_flows=300)
     with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 25, max_flows=1 << 12) as p:
         assert_same(p.parse(tr), oracle.parse(tr), p.flows())
