@@ -108,3 +108,34 @@ def test_multiflow_generator_flow_count(oracle):
     assert len(rec) == 20000
     assert len(table) == 100
     assert int(table["bytes"].sum()) == int(tr.caplen.sum())
+
+
+def test_exchange_calls_validate_before_device_work():
+    """The context-free exchange entry points refuse bad arguments with
+    TCBEE_EINVAL before touching a device (no GPU needed)."""
+    import ctypes as C
+    L = tcbee_amd.lib()
+    buf = (C.c_uint64 * 8)()
+    ids = (C.c_uint32 * 8)()
+    p, q = C.cast(buf, C.c_void_p), C.cast(ids, C.c_void_p)
+    q2 = C.c_void_p(C.addressof(ids) + 4)
+    E = _lib.EINVAL
+    # global ids: rank >= world, world 0, n_stride 1, gbase in == out, NULL arrays
+    assert L.tcbee_global_ids_device(p, p, 2, 2, 2, 4, q, 8, None, None, None) == E
+    assert L.tcbee_global_ids_device(p, p, 2, 0, 0, 4, q, 8, None, None, None) == E
+    assert L.tcbee_global_ids_device(p, p, 1, 2, 0, 4, q, 8, None, None, None) == E
+    assert L.tcbee_global_ids_device(p, p, 2, 2, 0, 4, q, 8, p, p, None) == E
+    assert L.tcbee_global_ids_device(None, p, 2, 2, 0, 4, q, 8, None, None, None) == E
+    assert L.tcbee_global_ids_device(p, p, 2, 2, 0, 4, None, 8, None, None, None) == E
+    # owner return / apply: world 0, seg_cap 0, NULL buffers, a map length without a map
+    assert L.tcbee_owner_return_device(q, p, 0, 4, q, 8, q2, None) == E
+    assert L.tcbee_owner_return_device(q, p, 2, 0, q, 8, q2, None) == E
+    assert L.tcbee_owner_return_device(None, p, 2, 4, q, 8, q2, None) == E
+    assert L.tcbee_owner_return_device(q, p, 2, 4, None, 8, q2, None) == E
+    assert L.tcbee_owner_apply_device(q, q, p, 0, 4, q2, 8, None) == E
+    assert L.tcbee_owner_apply_device(q, q, None, 2, 4, q2, 8, None) == E
+    assert L.tcbee_owner_apply_device(q, q, p, 2, 4, None, 8, None) == E
+    # context calls with no context
+    assert L.tcbee_owner_bucket_device(None, 2, 4, 8, p, q, p, None) == E
+    assert L.tcbee_flow_first_seen_device(None, p, 4, p, None) == E
+    assert L.tcbee_flow_first_frames_device(None, p, 4, p, None, p, 4, 4, None) == E
