@@ -445,7 +445,7 @@ def cgroup_cpus():
         return None
 
 
-def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=5, threads=None):
+def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=9, threads=None):
     """End-to-end rates from host memory: frames in pageable host RAM -> records +
     flow ids back in pageable host RAM (H2D and D2H inside the timed region).
       pipe_window64: tcbee_pipe, header-window staging (frame bytes [12, 76): one
@@ -683,6 +683,17 @@ def main():
             out["config3_zipf"] = {"mpkts": round(args.frames * args.steps / z_el / 1e6, 1),
                                    "ms_per_step": round(z_el / args.steps * 1e3, 4),
                                    "k1_ms": round(z_k1, 4), "zipf_s": 1.1, "check": z_chk}
+            # the IPv6 path at the same scale: 100M IPv6/TCP frames (78/576/1500 IMIX:
+            # IPv6 needs 74 header bytes), 10k flows; K1 loads the IPv6 tail chunk
+            v_el, v_k1, v_n, v_chk, _ = run_device(torch, None, 0, 1, args.frames, "imix6", 3,
+                                                args.flows, args.steps, args.warmup, args.seed,
+                                                full_check=not args.sample_check)
+            v_alg = IDX_BYTES + 74 + OUT_BYTES
+            out["config3_ipv6"] = {"mpkts": round(args.frames * args.steps / v_el / 1e6, 1),
+                                   "ms_per_step": round(v_el / args.steps * 1e3, 4),
+                                   "k1_ms": round(v_k1, 4), "alg_bytes_per_frame": v_alg,
+                                   "k1_alg_GBs": round(args.frames * v_alg / v_k1 / 1e6, 1),
+                                   "check": v_chk}
             # steady state of a recorder: the same frames with the table kept across
             # steps (every flow known: K1 hits only, K2 ranks nothing new)
             w_el, w_k1, w_n, w_chk, _ = run_device(torch, None, 0, 1, args.frames, args.sizes, 1,

@@ -354,8 +354,9 @@ int tcbee_ctx_profile_read(tcbee_ctx* ctx, double* k1_ms_total, uint64_t* k1_lau
  * Fills the header bytes of frames whose offset/caplen are already on the
  * device (see DESIGN.md "Synthetic traces"); local frame j is global frame
  * first_index + j. kind 0 = config-2 single flow, kind 1 = multi-flow IPv4
- * (flow of frame i = splitmix64(seed + 0x1000 + i) % n_flows). Payload bytes are
- * left as they are (callers zero the arena). Asynchronous on stream. */
+ * (flow of frame i = splitmix64(seed + 0x1000 + i) % n_flows), kind 3 = the same
+ * flows over IPv6/TCP (74 header bytes). Payload bytes are left as they are
+ * (callers zero the arena). Asynchronous on stream. */
 int tcbee_gen_frames_device(uint8_t* arena_dev, const uint64_t* offset_dev,
                             const uint32_t* caplen_dev, uint64_t n,
                             uint64_t first_index, int kind, uint64_t n_flows,

@@ -971,8 +971,9 @@ int tcbee_ctx_profile_read(tcbee_ctx* c, double* ms_total, uint64_t* launches) {
 int tcbee_gen_frames_device(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
                             uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed,
                             void* stream) {
-  if ((n && (!arena || !off || !len)) || (kind != 0 && kind != 1)) return TCBEE_EINVAL;
-  if (kind == 1 && n_flows == 0) return TCBEE_EINVAL;
+  if ((n && (!arena || !off || !len)) || (kind != 0 && kind != 1 && kind != 3))
+    return TCBEE_EINVAL;
+  if (kind != 0 && n_flows == 0) return TCBEE_EINVAL;
   if (!n) return TCBEE_OK;
   TRY_HIP(launch_gen(arena, off, len, n, first_index, kind, n_flows, seed, (hipStream_t)stream));
   return TCBEE_OK;
@@ -1043,12 +1044,14 @@ int tcbee_gen_shard_index_device(uint64_t n_global, int world, int rank, int kin
 
 int tcbee_gen_frames_host(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
                           uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed) {
-  if ((n && (!arena || !off || !len)) || (kind != 0 && kind != 1)) return TCBEE_EINVAL;
-  if (kind == 1 && n_flows == 0) return TCBEE_EINVAL;
+  if ((n && (!arena || !off || !len)) || (kind != 0 && kind != 1 && kind != 3))
+    return TCBEE_EINVAL;
+  if (kind != 0 && n_flows == 0) return TCBEE_EINVAL;
+  const uint32_t hl = gen_header_len(kind);
   for (uint64_t i = 0; i < n; ++i) {
-    uint8_t h[54];
+    uint8_t h[kGenHdrMax];
     gen_header(h, first_index + i, len[i], kind, n_flows, seed);
-    std::memcpy(arena + off[i], h, len[i] < 54u ? len[i] : 54u);
+    std::memcpy(arena + off[i], h, len[i] < hl ? len[i] : hl);
   }
   return TCBEE_OK;
 }

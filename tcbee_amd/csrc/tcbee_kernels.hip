@@ -2176,9 +2176,10 @@ __global__ void k_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, 
                       const uint64_t* gidx, const uint64_t* zcdf) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
-    uint8_t h[54];
+    uint8_t h[kGenHdrMax];
     gen_header(h, gidx ? gidx[i] : first_index + i, len[i], kind, n_flows, seed, zcdf);
-    const uint32_t m = len[i] < 54u ? len[i] : 54u;
+    const uint32_t hl = gen_header_len(kind);
+    const uint32_t m = len[i] < hl ? len[i] : hl;
     uint8_t* dst = arena + off[i];
     for (uint32_t b = 0; b < m; ++b) dst[b] = h[b];
   }

@@ -26,6 +26,7 @@ DEFAULT_SEED = 0x7CBEE
 GEN_SINGLE = 0
 GEN_MULTI = 1
 GEN_ZIPF = 2     # config 3 "second run": flows drawn Zipf(ZIPF_S)
+GEN_MULTI_V6 = 3  # GEN_MULTI's flow draw over IPv6/TCP frames (74 header bytes)
 ZIPF_S = 1.1
 
 
@@ -97,15 +98,17 @@ def synth_index(n: int, sizes: str = "64", seed: int = DEFAULT_SEED, first_index
     """offset/caplen/ts_ns of a synthetic trace and its arena length.
 
     sizes="64": every frame 64 B (config 2); sizes="imix": 64/576/1500 at 7:4:1
-    drawn per frame from splitmix64(seed ^ 0x1M1X + i) % 12 (config 3/4).
+    drawn per frame from splitmix64(seed ^ 0x1M1X + i) % 12 (config 3/4);
+    sizes="imix6": the same draw with 78/576/1500 (IPv6/TCP needs 74 bytes).
     Frames are packed back to back (no padding), as in a capture file.
     """
     i = np.arange(first_index, first_index + n, dtype=np.uint64)
     if sizes == "64":
         caplen = np.full(n, 64, dtype=np.uint32)
-    elif sizes == "imix":
+    elif sizes in ("imix", "imix6"):
         r = splitmix64(np.uint64(seed ^ 0x1A1E) + i) % np.uint64(12)
-        caplen = np.where(r < 7, 64, np.where(r < 11, 576, 1500)).astype(np.uint32)
+        small = 64 if sizes == "imix" else 78
+        caplen = np.where(r < 7, small, np.where(r < 11, 576, 1500)).astype(np.uint32)
     else:
         raise ValueError(sizes)
     offset = np.zeros(n, dtype=np.uint64)

@@ -110,6 +110,18 @@ def test_multiflow_generator_flow_count(oracle):
     assert int(table["bytes"].sum()) == int(tr.caplen.sum())
 
 
+def test_ipv6_generator_flows(oracle):
+    """kind 3 (IPv6/TCP, IMIX6 sizes): every frame accepted as IPv6, the requested
+    flow count, addresses in the v6 record fields only."""
+    from tcbee_amd.trace import GEN_MULTI_V6
+    tr = tcbee_amd.synth_trace(20000, sizes="imix6", kind=GEN_MULTI_V6, n_flows=300)
+    assert int(tr.caplen.min()) == 78
+    rec, fh, fi, ctr, table = oracle.parse(tr)
+    assert len(rec) == 20000 and len(table) == 300
+    assert not rec[:, 8:16].any() and rec[:, 16:48].any()  # v4 fields 0, v6 set
+    assert int(table["bytes"].sum()) == int(tr.caplen.sum())
+
+
 def test_exchange_calls_validate_before_device_work():
     """The context-free exchange entry points refuse bad arguments with
     TCBEE_EINVAL before touching a device (no GPU needed)."""

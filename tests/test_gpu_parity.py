@@ -133,6 +133,13 @@ def test_config3_imix_multiflow(parser, oracle):
     assert_same(parser.parse(tr), oracle.parse(tr), parser.flows())
 
 
+def test_config3_ipv6_multiflow(parser, oracle):
+    """IPv6/TCP IMIX (kind 3): K1's IPv6 tail loads over a whole batch."""
+    tr = tcbee_amd.synth_trace(300_000, sizes="imix6", kind=3, n_flows=10_000)
+    parser.reset_flows()
+    assert_same(parser.parse(tr), oracle.parse(tr), parser.flows())
+
+
 def test_config3_zipf(parser, oracle):
     """Config 3's second run (Zipf s=1.1 flow mix): a hot head flow (~10 % of the
     records) and a long tail through the same kernels."""
@@ -143,7 +150,8 @@ def test_config3_zipf(parser, oracle):
 
 def test_device_generator_matches_host(gpu):
     import torch
-    for sizes, kind, nf in [("64", 0, 1), ("imix", 1, 777), ("imix", 2, 10_000), ("64", 2, 1)]:
+    for sizes, kind, nf in [("64", 0, 1), ("imix", 1, 777), ("imix", 2, 10_000), ("64", 2, 1),
+                            ("imix6", 3, 5000)]:
         n = 100_000
         off, ln, ts, alen = tcbee_amd.synth_index(n, sizes=sizes)
         host = tcbee_amd.synth_trace(n, sizes=sizes, kind=kind, n_flows=nf)

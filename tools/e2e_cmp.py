@@ -1,5 +1,6 @@
-"""Same box: bench.host_e2e (torch imported, as in bench.py) twice, with the
-cgroup's CPU throttling (cpu.stat) over each run."""
+"""Same box: bench.host_e2e (as in bench.py) in different process states:
+before torch touches the GPU, after torch's CUDA init, after a device-resident
+bench leg — with the cgroup's CPU throttling (cpu.stat) over each run."""
 import json
 import os
 import sys
@@ -16,9 +17,21 @@ def cpu_stat():
         return {}
 
 
-for thr in (16, 12, 16, 12):
+def run(tag):
     a = cpu_stat()
-    r = bench.host_e2e("imix", 1, 10_000, 0x7CBEE, threads=thr)
+    r = bench.host_e2e("imix", 1, 10_000, 0x7CBEE)
     b = cpu_stat()
-    r["cpu_stat_delta"] = {k: int(b[k]) - int(a[k]) for k in b if k in a}
-    print(json.dumps(r), flush=True)
+    print(tag, {k: v["mpkts"] for k, v in r.items() if isinstance(v, dict) and "mpkts" in v},
+          "throttled_usec", int(b.get("throttled_usec", 0)) - int(a.get("throttled_usec", 0)),
+          flush=True)
+
+
+run("fresh")
+import torch  # noqa: E402
+torch.zeros(1, device="cuda")
+torch.cuda.synchronize()
+run("torch-cuda")
+torch.cuda.set_stream(torch.cuda.Stream())
+bench.run_device(torch, None, 0, 1, 20_000_000, "imix", 1, 10_000, 5, 2, 0x7CBEE)
+run("after-device-leg")
+run("again")
