@@ -37,7 +37,7 @@ def main():
                "imix1M": ("imix", 1, 1_000_000), "64B10k": ("64", 1, 10_000),
                "imix125k": ("imix", 1, 125_000), "imix20k": ("imix", 1, 20_000),
                "imix30k": ("imix", 1, 30_000), "imix45k": ("imix", 1, 45_000),
-               "imix60k": ("imix", 1, 60_000)}
+               "imix60k": ("imix", 1, 60_000), "imix6v6": ("imix6", 3, 10_000)}
     results = {}
     for wl in args.workloads.split(","):
         sizes, kind, nf = wl_defs[wl]
