@@ -7,12 +7,14 @@ Workload (config 3 of BASELINE.json, the largest single-GPU config): per GPU,
 ``tcbee_parse_batch_device`` over the whole batch: parse + 74-B records +
 flow hash + flow classification (table upsert, dense first-seen ids) +
 counters. Each step is one fresh trace (the flow table starts empty). With
---gpus N each rank parses its own contiguous shard of one global trace (weak
-scaling, no frame exchange); per step the compact per-rank flow tables are
-all-gathered over RCCL, merged on every GPU (global dense first-seen ids) and
-each rank's record flow ids are remapped; the counters are all-reduced. That
-exchange runs on a side stream and overlaps the next step's parse (two output
-slots; tcbee_amd.dist.OverlappedMerge); the timed region ends after all of it.
+--gpus N (weak scaling, no frame exchange) each rank parses its flow-hash shard
+of one global trace of N x --frames frames (north_star's partition, the NIC-RSS
+view): between K2 and K3 one RCCL all-gather of every rank's first-frame array
+gives the global dense first-seen ids, which K3 writes directly
+(tcbee_amd.dist.FlowHashExchange); the counters are all-reduced; the timed region
+ends after all of it. --shard contig: contiguous shards, each flow merged at its
+hash owner (OwnerExchange; TCBEE_BENCH_EXCHANGE=merge: the all-gather merge
+overlapped with the next parse, OverlappedMerge).
 
 Prints ONE JSON line (rank 0). See DESIGN.md "Measurement".
 """
