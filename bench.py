@@ -38,8 +38,13 @@ V4_HDR_BYTES = 54              # eth + ipv4 + tcp header bytes the hook reads
 OUT_BYTES = 74 + 4 + 4         # record + flow hash + flow id (slot) written per record
 
 
+_T0 = time.perf_counter()
+
+
 def log(*a):
-    print(*a, file=sys.stderr, flush=True)
+    """Progress on stderr (the JSON line alone goes to stdout): every leg and every
+    long check reports, so a multi-minute default run is never silent."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s]", *a, file=sys.stderr, flush=True)
 
 
 def build_device_trace(torch, n, sizes, kind, n_flows, seed, first_index, stream):
@@ -93,6 +98,8 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
                multi=None, full_check=False, flowhash=False, vworld=0, warm=False):
     import tcbee_amd
     stream = torch.cuda.current_stream().cuda_stream
+    log(f"rank {rank}: building {n} frames ({sizes}, {n_flows} flows, "
+        f"{'flow-hash' if flowhash else 'contiguous'} shard)")
     # multi: the N>1 exchange runs (also at N=1 under TCBEE_BENCH_FORCE_MERGE=1, a
     # one-GPU rehearsal of its cost and of the overlap)
     multi = world > 1 if multi is None else multi
@@ -216,6 +223,7 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
             fm.step(b["id"], b["n"], n, stream=stream)
             dist.all_reduce(b["ctr"])
 
+    log(f"rank {rank}: {n} frames resident; {warmup} warm-up + {steps} timed steps")
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -237,6 +245,7 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     t1 = time.perf_counter()
     k1_ms, k1_launches = p.profile_read()
     elapsed = t1 - t0
+    log(f"rank {rank}: {steps} steps in {elapsed * 1e3:.1f} ms; validating")
     fx_ms = fx.exchange_ms() if fx is not None else None
     status = p.status()
 
@@ -350,6 +359,8 @@ def validate_full(torch, d_rec, d_hash, d_id, n, sizes, kind, n_flows, seed, nre
             if not same and bad_at is None:
                 bad_at = lo
             ok = ok and same
+            if (lo // chunk) % 10 == 9:
+                log(f"full check: {hi}/{n} records ({time.perf_counter() - t0:.0f}s)")
         table = orc.flows(ft)
     finally:
         orc.free_flowtab(ft)
@@ -394,6 +405,7 @@ def cpu_baseline(sizes, kind, n_flows, seed, seconds, threads, sample_n=2_000_00
     tr = tcbee_amd.synth_trace(sample_n, sizes=sizes, kind=kind, n_flows=n_flows, seed=seed)
     out = {}
     for t in sorted({1, threads}):
+        log(f"cpu baseline: {t} thread(s)")
         done, t0 = 0, time.perf_counter()
         while True:
             orc.baseline(tr, threads=t)
@@ -462,11 +474,13 @@ def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=9, threads=None):
     # beat 16 in every paired run (521-556 vs 324-472 Mpkt/s, tools/e2e_cmp.py);
     # the gather is host-memory bound, not CPU bound (no cgroup throttling seen)
     threads = threads or max(4, host_cores() * 3 // 4)
+    log(f"e2e: generating {n} frames on the host")
     tr = tcbee_amd.synth_trace(n, sizes=sizes, kind=kind, n_flows=n_flows, seed=seed)
     rec = np.empty((n, 74), np.uint8)
     ids = np.empty(n, np.uint32)
     out = {"frames": n, "threads": threads, "arena_bytes": int(len(tr.arena))}
     for name, window in (("pipe_window64", 64), ("pipe_window80", 80), ("pipe_whole", 0)):
+        log(f"e2e: {name}")
         with Pipeline(device=0, chunk_frames=1 << 20, window=window, depth=4, threads=threads,
                       chunk_bytes=(1 << 29), max_flows=max(4 * n_flows, 1 << 12)) as p:
             p.run(tr, out_rec=rec, out_id=ids)  # warm-up: pinned staging, first touches
@@ -513,6 +527,7 @@ def config5_replay(seed, n=1_000_000, n_flows=4, threads=None):
     from tcbee_amd.pipeline import replay_pcap
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_py import Oracle
+    log("config 5: pcap replay")
     tr = tcbee_amd.synth_trace(n, sizes="64", kind=1 if n_flows > 1 else 0, n_flows=n_flows,
                                seed=seed)
     d = tempfile.mkdtemp(prefix="tcbee_c5_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
@@ -743,6 +758,7 @@ def main():
                 "single_thread_file": round(res["file"][0], 2),
                 "file_sample": "1 thread, records appended to tmpfs xdp.tcp through a 720000-B "
                                "buffer (handlers/mod.rs:70-139)"}
+        log("done")
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
