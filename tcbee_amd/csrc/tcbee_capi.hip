@@ -55,6 +55,7 @@ struct tcbee_ctx {
   uint32_t* d_k3_region = nullptr;   // K3 mode 1 (tables with > kCountBins slots only)
   uint32_t* d_k3_offs = nullptr;
   uint64_t* d_k3_lpart = nullptr;
+  uint32_t* d_k3_coffs = nullptr;    // k_count_chunk: bucket offsets per kChunk records
   uint32_t k3_nb_max = 0, k3_g2 = 0;
   uint64_t k3_g1max = 0, part_words = 0;
   int n_cu = 256;
@@ -209,6 +210,7 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
   dfree(c->d_k3_region);
   dfree(c->d_k3_offs);
   dfree(c->d_k3_lpart);
+  dfree(c->d_k3_coffs);
   dfree(c->d_arena);
   dfree(c->d_off);
   dfree(c->d_len);
@@ -331,6 +333,11 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
     if ((e = dalloc(&c->d_k3_offs, 2ull * c->n_cu * (c->k3_nb_max + 1))) != hipSuccess)
       return fail(map_err(e));
     if ((e = dalloc(&c->d_k3_lpart, 2ull * c->k3_g2 * kBucket)) != hipSuccess)
+      return fail(map_err(e));
+    // single-pass chunked scatter (batches of <= kSmallNb buckets): offsets of every
+    // chunk's buckets (4 B x 513 per 16384 frames)
+    if ((e = dalloc(&c->d_k3_coffs, ((max_frames + kChunk - 1) / kChunk + 1) * (kSmallNb + 1))) !=
+        hipSuccess)
       return fail(map_err(e));
   }
   rc = tcbee_flow_reset(c);
@@ -508,6 +515,8 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     k.offs = c->d_k3_offs;
     k.nb_max = c->k3_nb_max;
     k.lpart = c->d_k3_lpart;
+    k.coffs = c->d_k3_coffs;
+    k.chunk_off = c->k3_variant == 91 ? 1u : 0u;  // TCBEE_K3ABL=91: the two-pass scatter (A/B)
     // trade-off: more blocks = more latency hidden; each block writes a partial row
     // of every flow, so a block should see a few thousand records; and a block
     // never covers more than kK3MaxPer records (bin fields cannot overflow)

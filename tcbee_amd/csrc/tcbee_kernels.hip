@@ -1574,9 +1574,15 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
 
 // Mode 1, phase 1 as its own launch: 32 KiB of LDS, so two workgroups share a CU
 // (k_count's 144 KiB of bins + map allow one).
+// the single-pass chunked scatter (k_count_chunk) takes every mode-1 batch of up to
+// kSmallNb buckets when the context has its chunk offsets
+__device__ __forceinline__ bool chunk_scatter(const CountArgs& c, uint64_t nflows) {
+  const uint64_t nb = (nflows + kBucket - 1) >> kBucketBits;
+  return c.coffs != nullptr && !c.chunk_off && nb <= kSmallNb;
+}
 __device__ __forceinline__ bool staged_scatter(const CountArgs& c, uint64_t nflows) {
   const uint64_t nb = (nflows + kBucket - 1) >> kBucketBits;
-  return !c.scatter_unstaged && nb >= kStagedMinNb && nb <= kSmallNb;
+  return !c.scatter_unstaged && nb >= kStagedMinNb && nb <= kSmallNb && !chunk_scatter(c, nflows);
 }
 
 template <int U, bool PACK, int SABL = 0>
@@ -1585,7 +1591,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count_scatter(CountArgs c) {
   __shared__ uint32_t s_w[kCountBlock / 64];
   const uint64_t nflows = c.batch->flow_total;
   if (count_mode(c, nflows) != 1) return;
-  if (staged_scatter(c, nflows)) return;  // k_count_scatter_staged
+  if (staged_scatter(c, nflows) || chunk_scatter(c, nflows)) return;  // the other two
   const uint64_t n_acc = c.batch->n_acc;
   const uint64_t per = count_per(n_acc, gridDim.x);
   const uint64_t lo = (uint64_t)blockIdx.x * per < n_acc ? (uint64_t)blockIdx.x * per : n_acc;
@@ -1613,6 +1619,119 @@ __global__ __launch_bounds__(kCountBlock) void k_count_scatter_staged(CountArgs 
   count_scatter<U, PACK, 0, true>(c, lo, hi, nflows, s_hist, s_cur, s_w, st);
 }
 
+// Mode 1, single pass (nb <= kSmallNb): each workgroup takes chunks of kChunk
+// accepted records (16 per thread) and
+//  1. ranks them by bucket in LDS (counts per bucket, one LDS add per record or one
+//     per wave when the wave's records share a bucket; no-flow records go to a
+//     spare bucket nb), scans the counts;
+//  2. places every record's region entry (claim within the bucket | caplen) and its
+//     chunk position + bucket at its bucket-sorted slot in LDS;
+//  3. walks the sorted entries with consecutive lanes on consecutive entries: the
+//     region entry is stored coalesced at region[chunk + idx] (the chunk's buckets
+//     are contiguous runs; coffs[q] = their offsets for k_count_bucket) and the
+//     claim -> output id gather reads omap inside one bucket's 16 KiB window per
+//     wave (L1-local), where the record-order gather of the two-pass scatter hit 64
+//     random lines of a table of every flow;
+//  4. writes each id back to its record position in LDS and stores the chunk's ids
+//     in record order, coalesced.
+// One pass over the K1 -> K3 words, no per-block cursors, no scattered stores.
+template <bool PACK>
+__global__ __launch_bounds__(kCountBlock) void k_count_chunk(CountArgs c) {
+  constexpr int U = kChunk / kCountBlock;
+  __shared__ uint32_t s_ent[kChunk];   // region entries, bucket-sorted; then ids by position
+  __shared__ uint32_t s_pb[kChunk];    // chunk position | bucket << 14 of each sorted entry
+  __shared__ uint32_t s_ch[kSmallNb + 1], s_co[kSmallNb + 1];
+  __shared__ uint32_t s_w[kCountBlock / 64];
+  static_assert(kChunk == kK3Gran && kChunk <= (1u << 14) && kSmallNb < (1u << 18), "layout");
+  const uint64_t nflows = c.batch->flow_total;
+  if (count_mode(c, nflows) != 1 || !chunk_scatter(c, nflows)) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);  // spare bucket: nb
+  const uint64_t n_acc = c.batch->n_acc;
+  const uint64_t nchunks = (n_acc + kChunk - 1) / kChunk;
+  for (uint64_t q = blockIdx.x; q < nchunks; q += gridDim.x) {
+    const uint64_t base = q * kChunk;
+    const uint64_t hi = base + kChunk < n_acc ? base + kChunk : n_acc;
+    const uint32_t nval = (uint32_t)(hi - base);
+    for (uint32_t b = tid; b <= nb; b += kCountBlock) s_ch[b] = 0;
+    uint32_t ent[U], bk[U], lp[U];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // two halves of U / 2 loads (register pressure)
+      constexpr int H = U / 2;
+      uint32_t cl[H], len[H];
+      load_acc<H, PACK>(c, base + (uint64_t)h * H * kCountBlock + tid, base, hi, cl, len);
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        const bool big = len[k] >= kRegLenEsc;
+        bk[h * H + k] = cl[k] != 0xFFFFFFFFu ? (cl[k] >> kBucketBits) : nb;
+        ent[h * H + k] = (cl[k] & (kBucket - 1u)) | ((big ? 0u : len[k]) << kBucketBits);
+        if (big && cl[k] != 0xFFFFFFFFu)
+          atomicAdd((unsigned long long*)&c.cnt[2ull * c.cmap[cl[k]] + 1], (unsigned long long)len[k]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const bool valid = (uint32_t)k * kCountBlock + tid < nval;
+      const uint32_t b0 = __builtin_amdgcn_readfirstlane(bk[k]);
+      const uint64_t vm = __ballot(valid);
+      if (__all(!valid || bk[k] == b0)) {
+        // one add for the wave (a hot flow's bucket): ranks in lane order
+        uint32_t r0 = 0;
+        if (lane == 0 && vm) r0 = atomicAdd(&s_ch[b0], (uint32_t)__popcll(vm));
+        r0 = __shfl(r0, 0);
+        lp[k] = r0 + (uint32_t)__popcll(vm & lanemask_lt());
+      } else {
+        lp[k] = valid ? atomicAdd(&s_ch[bk[k]], 1u) : 0u;
+      }
+    }
+    __syncthreads();
+    {
+      uint32_t tot;
+      const uint32_t off = block1024_excl_scan(tid <= nb ? s_ch[tid] : 0u, s_w, tot);
+      if (tid <= nb) s_co[tid] = off;
+      if (tid <= nb) c.coffs[q * (kSmallNb + 1) + tid] = off;  // [nb] = end of the real buckets
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint32_t pos = (uint32_t)k * kCountBlock + tid;
+      if (pos >= nval) continue;
+      const uint32_t idx = s_co[bk[k]] + lp[k];
+      s_ent[idx] = ent[k];
+      s_pb[idx] = pos | (bk[k] << 14);
+    }
+    __syncthreads();
+    uint32_t id[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint32_t idx = (uint32_t)k * kCountBlock + tid;
+      id[k] = 0xFFFFFFFFu;
+      if (idx >= nval) continue;
+      const uint32_t e = s_ent[idx], b = s_pb[idx] >> 14;
+      if (b < nb) {
+        c.region[base + idx] = e;  // consecutive lanes, consecutive entries
+        id[k] = c.omap[(b << kBucketBits) | (e & (kBucket - 1u))];
+      }
+    }
+    __syncthreads();  // every sorted entry read: s_ent becomes the id array
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint32_t idx = (uint32_t)k * kCountBlock + tid;
+      if (idx < nval) s_ent[s_pb[idx] & (kChunk - 1u)] = id[k];
+    }
+    __syncthreads();
+    if (c.out_id) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
+        if (p < hi && p < c.out_cap) __builtin_nontemporal_store(s_ent[(uint32_t)k * kCountBlock + tid], &c.out_id[p]);
+      }
+    }
+    __syncthreads();  // before the next chunk reuses s_ch / s_ent
+  }
+}
+
 // Mode 1, phase 2: workgroup (j, s) histograms bucket j over the segments of K3
 // blocks s, s+S, ... (S = gridDim / nb) in LDS; each wave walks one block's
 // segment at a time, 4 records per lane in flight. Writes a dense partial row.
@@ -1628,12 +1747,17 @@ __global__ __launch_bounds__(kCountBlock) void k_count_bucket(CountArgs c, uint3
   for (uint32_t t = tid; t < kBucket; t += kCountBlock) s_pk[t] = s_by[t] = 0;
   __syncthreads();
   const uint64_t n_acc = c.batch->n_acc;
-  const uint64_t per = count_per(n_acc, g1);
+  // segments: the two-pass scatter's g1 blocks, or k_count_chunk's chunks
+  const bool chunked = chunk_scatter(c, nflows);
+  const uint64_t per = chunked ? (uint64_t)kChunk : count_per(n_acc, g1);
+  const uint64_t G = chunked ? (n_acc + kChunk - 1) / kChunk : g1;
+  const uint32_t* obase = chunked ? c.coffs : c.offs;
+  const uint64_t ostride = chunked ? kSmallNb + 1 : c.nb_max + 1;
   constexpr uint32_t kWaves = kCountBlock / 64;
-  for (uint32_t q = s + S * wave; q < g1; q += S * kWaves) {
-    const uint64_t lo_q = (uint64_t)q * per;
+  for (uint64_t q = s + S * wave; q < G; q += S * kWaves) {
+    const uint64_t lo_q = q * per;
     if (lo_q >= n_acc) break;
-    const uint32_t* o = c.offs + (uint64_t)q * (c.nb_max + 1);
+    const uint32_t* o = obase + q * ostride;
     const uint64_t a0 = lo_q + o[j], a1 = lo_q + o[j + 1];
     for (uint64_t x = a0 + lane; x < a1; x += 256) {
       uint32_t v[4];
@@ -2415,9 +2539,14 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
         if (c.pack_bits) hipLaunchKernelGGL((k_count_scatter<8, true>), gs, dim3(kCountBlock), 0, s, c);
         else hipLaunchKernelGGL((k_count_scatter<8, false>), gs, dim3(kCountBlock), 0, s, c);
     }
-    // (each of the two returns at once unless the table's bucket count is its own)
+    // (each of the three returns at once unless the batch's bucket count is its own)
     if (c.pack_bits) hipLaunchKernelGGL((k_count_scatter_staged<4, true>), gs, dim3(kCountBlock), 0, s, c);
     else hipLaunchKernelGGL((k_count_scatter_staged<4, false>), gs, dim3(kCountBlock), 0, s, c);
+    if (c.coffs) {  // 132 KiB of LDS: one workgroup per CU (g1s is up to two per CU)
+      const dim3 gc((g1s + 1) / 2);
+      if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk<true>), gc, dim3(kCountBlock), 0, s, c);
+      else hipLaunchKernelGGL((k_count_chunk<false>), gc, dim3(kCountBlock), 0, s, c);
+    }
     hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1s);
   }
   // mode 0 needs kCountBins threads; mode 1 up to nb_max * kBucket (grid-stride)

@@ -571,3 +571,44 @@ def test_async_ids_stream_batches(gpu, oracle, reset, flows):
             oracle.free_flowtab(ft)
         assert np.array_equal(p.flows(), table)
         assert p.status() == 0
+
+
+def _concat(a, b):
+    """Trace a followed by trace b (b's offsets rebased past a's arena)."""
+    return Trace(np.concatenate([a.arena, b.arena]),
+                 np.concatenate([a.offset, b.offset + np.uint64(len(a.arena))]),
+                 np.concatenate([a.caplen, b.caplen]), np.concatenate([a.ts_ns, b.ts_ns]))
+
+
+@pytest.mark.parametrize("variant", ["0", "91"])
+@pytest.mark.parametrize("flows", [40_000, 150_000])
+def test_k3_chunked_scatter(gpu, oracle, variant, flows, monkeypatch):
+    """K3 mode 1's single-pass chunked scatter (k_count_chunk: chunks of 16384
+    records bucket-sorted in LDS, ids gathered bucket by bucket, region runs per
+    chunk) and the two-pass scatter it replaced (TCBEE_K3ABL=91), bit-exact vs the
+    oracle: a ragged last chunk, caplens past the 20-bit region field and the
+    packed K1 -> K3 field, a single-flow stretch (every wave on one bucket), two
+    batches (claims of batch 1 looked up again in batch 2)."""
+    from tracegen import mixed_trace
+    monkeypatch.setenv("TCBEE_TEST_K3_NORANGE", "1")
+    monkeypatch.setenv("TCBEE_K3ABL", variant)
+    mt = mixed_trace(350_001, seed=123, n_flows=flows)
+    rng = np.random.default_rng(9)
+    big = rng.choice(mt.n, size=200, replace=False)
+    pad = 2_600_000
+    ln = mt.caplen.copy()
+    ln[big] = rng.integers(16_000, pad, size=len(big)).astype(np.uint32)
+    mt = Trace(np.concatenate([mt.arena, np.zeros(pad, np.uint8)]), mt.offset, ln, mt.ts_ns)
+    tr = _concat(mt, tcbee_amd.synth_trace(70_000, sizes="64", kind=0, n_flows=1))
+    cut = 150_000
+    with tcbee_amd.PacketParser(max_frames=1 << 19, max_arena=1 << 28, max_flows=1 << 18) as p:
+        r1 = p.parse(tr.slice(0, cut))
+        assert p.count_mode() == 1
+        r2 = p.parse(tr.slice(cut, tr.n))
+        assert p.count_mode() == 1
+        rec, fh, fi, ctr, table = oracle.parse(tr)
+        assert np.array_equal(np.concatenate([r1.records, r2.records]), rec)
+        assert np.array_equal(np.concatenate([r1.flow_id, r2.flow_id]), fi)
+        fl = p.flows()
+        assert len(fl) == len(table) and np.array_equal(fl, table)
+        assert p.status() == 0
