@@ -336,7 +336,7 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
       return fail(map_err(e));
     // single-pass chunked scatter (batches of <= kSmallNb buckets): offsets of every
     // chunk's buckets (4 B x 513 per 16384 frames)
-    if ((e = dalloc(&c->d_k3_coffs, ((max_frames + kChunk - 1) / kChunk + 1) * (kSmallNb + 1))) !=
+    if ((e = dalloc(&c->d_k3_coffs, ((max_frames + kChunkMin - 1) / kChunkMin + 1) * (kChunkMaxNb + 1))) !=
         hipSuccess)
       return fail(map_err(e));
   }
@@ -517,6 +517,10 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     k.lpart = c->d_k3_lpart;
     k.coffs = c->d_k3_coffs;
     k.chunk_off = c->k3_variant == 91 ? 1u : 0u;  // TCBEE_K3ABL=91: the two-pass scatter (A/B)
+    // 16384-record chunks (1024 threads, one workgroup per CU); TCBEE_K3ABL=92: 8192
+    // (512 threads, two per CU) — measured slower: 125k flows 5.60 vs 5.72 ms/step,
+    // 1M flows 7.51 vs 7.77 (shorter bucket runs for k_count_bucket, twice the chunks)
+    k.chunk = c->k3_variant == 92 ? 8192u : 16384u;
     // trade-off: more blocks = more latency hidden; each block writes a partial row
     // of every flow, so a block should see a few thousand records; and a block
     // never covers more than kK3MaxPer records (bin fields cannot overflow)

@@ -139,6 +139,8 @@ struct CountArgs {
   // bucket offsets inside chunk q (row stride kSmallNb + 1). nullptr: not used
   uint32_t* coffs;
   uint32_t chunk_off;        // 1: the two-pass scatter instead (A/B hook, TCBEE_K3ABL=91)
+  uint32_t chunk;            // records per chunk: 16384 (1024 threads, one workgroup per
+                             // CU) or 8192 (512 threads, two per CU; TCBEE_K3ABL=92, A/B)
 };
 // g1 = k_count blocks; g1s = k_count_scatter blocks; g2 = k_count_bucket blocks
 // (g2 = 0: mode 1 impossible, neither is launched)
@@ -272,10 +274,12 @@ constexpr uint32_t kMaxBuckets = 4096;    // mode 1 up to 16M flows (hist + curs
 // 125k (31) +0.09 and 60k (15) +0.16 ms, where a wave's lanes already hit few
 // bucket cursors and the per-chunk barriers cost more than they save
 constexpr uint32_t kSmallNb = 512, kStagedMinNb = 64;
-// k_count_chunk's chunk: the records one 1024-thread workgroup sorts by bucket in
-// LDS at a time (16 per thread); = kK3Gran, so the bucket pass sees chunk q as the
-// segment [q * kChunk, (q + 1) * kChunk)
-constexpr uint32_t kChunk = 16384;
+// k_count_chunk's chunk: the records one workgroup sorts by bucket in LDS at a time
+// (16 per thread); the bucket pass sees chunk q as the segment [q * chunk, (q+1) * chunk)
+constexpr uint32_t kChunkMin = 8192;
+// chunked mode up to kChunkMaxNb - 1 buckets: the scan of nb + 1 counts takes one
+// per thread of the smaller (512-thread) workgroup
+constexpr uint32_t kChunkMaxNb = 511;
 constexpr uint64_t kMaxTableFlows = 1ull << 24;  // tcbee_ctx_create's max_flows limit
 // mode-1 region entry: caplens from kRegLenEsc up are stored as 0 and their bytes
 // added to the flow's counter by a global atomic (frames of >= 1 MiB: never on a

@@ -1158,20 +1158,20 @@ __device__ __forceinline__ int count_mode(const CountArgs& c, uint64_t nflows) {
 // others give claim ~0, len 0): claim (~0: no flow) and caplen, packed in one
 // word when the context's table is small enough (pack_bits != 0). All words are
 // loaded before any is inspected (a branch between them would serialize them).
-template <int U, bool PACK>
+template <int U, bool PACK, int STRIDE = kCountBlock>
 __device__ __forceinline__ void load_acc(const CountArgs& c, uint64_t p0, uint64_t lo, uint64_t hi,
                                          uint32_t (&claim)[U], uint32_t (&len)[U]) {
   uint32_t v[U];
 #pragma unroll
   for (int k = 0; k < U; ++k) {
-    const uint64_t p = p0 + (uint64_t)k * kCountBlock;
+    const uint64_t p = p0 + (uint64_t)k * STRIDE;
     v[k] = __builtin_nontemporal_load(&c.acc_flow[p < hi ? p : lo]);
     if (!PACK) len[k] = __builtin_nontemporal_load(&c.acc_len[p < hi ? p : lo]);
   }
   const uint32_t lmax = 0xFFFFFFFFu >> c.pack_bits;
 #pragma unroll
   for (int k = 0; k < U; ++k) {
-    const uint64_t p = p0 + (uint64_t)k * kCountBlock;
+    const uint64_t p = p0 + (uint64_t)k * STRIDE;
     if (PACK) {
       claim[k] = v[k] == 0xFFFFFFFFu ? v[k] : (v[k] & ((1u << c.pack_bits) - 1u));
       len[k] = v[k] >> c.pack_bits;
@@ -1183,7 +1183,7 @@ __device__ __forceinline__ void load_acc(const CountArgs& c, uint64_t p0, uint64
   if (PACK) {
 #pragma unroll
     for (int k = 0; k < U; ++k)
-      if (len[k] == lmax && claim[k] != 0xFFFFFFFFu) len[k] = c.acc_len[p0 + (uint64_t)k * kCountBlock];
+      if (len[k] == lmax && claim[k] != 0xFFFFFFFFu) len[k] = c.acc_len[p0 + (uint64_t)k * STRIDE];
   }
 }
 
@@ -1200,6 +1200,7 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
 }
 
 // exclusive scan over the 1024 threads of a block; s_w: 16 words of LDS
+template <int NT = kCountBlock>
 __device__ __forceinline__ uint32_t block1024_excl_scan(uint32_t v, uint32_t* s_w, uint32_t& total) {
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   uint32_t x = v;
@@ -1213,7 +1214,7 @@ __device__ __forceinline__ uint32_t block1024_excl_scan(uint32_t v, uint32_t* s_
   uint32_t base = 0;
   total = 0;
 #pragma unroll
-  for (int w = 0; w < kCountBlock / 64; ++w) {
+  for (int w = 0; w < NT / 64; ++w) {
     const uint32_t t = s_w[w];
     if ((uint32_t)w < wave) base += t;
     total += t;
@@ -1575,10 +1576,10 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
 // Mode 1, phase 1 as its own launch: 32 KiB of LDS, so two workgroups share a CU
 // (k_count's 144 KiB of bins + map allow one).
 // the single-pass chunked scatter (k_count_chunk) takes every mode-1 batch of up to
-// kSmallNb buckets when the context has its chunk offsets
+// kChunkMaxNb - 1 buckets when the context has its chunk offsets
 __device__ __forceinline__ bool chunk_scatter(const CountArgs& c, uint64_t nflows) {
   const uint64_t nb = (nflows + kBucket - 1) >> kBucketBits;
-  return c.coffs != nullptr && !c.chunk_off && nb <= kSmallNb;
+  return c.coffs != nullptr && !c.chunk_off && nb < kChunkMaxNb;
 }
 __device__ __forceinline__ bool staged_scatter(const CountArgs& c, uint64_t nflows) {
   const uint64_t nb = (nflows + kBucket - 1) >> kBucketBits;
@@ -1619,7 +1620,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count_scatter_staged(CountArgs 
   count_scatter<U, PACK, 0, true>(c, lo, hi, nflows, s_hist, s_cur, s_w, st);
 }
 
-// Mode 1, single pass (nb <= kSmallNb): each workgroup takes chunks of kChunk
+// Mode 1, single pass (nb < kChunkMaxNb): each workgroup takes chunks of c.chunk
 // accepted records (16 per thread) and
 //  1. ranks them by bucket in LDS (counts per bucket, one LDS add per record or one
 //     per wave when the wave's records share a bucket; no-flow records go to a
@@ -1635,16 +1636,18 @@ __global__ __launch_bounds__(kCountBlock) void k_count_scatter_staged(CountArgs 
 //  4. writes each id back to its record position in LDS and stores the chunk's ids
 //     in record order, coalesced.
 // One pass over the K1 -> K3 words, no per-block cursors, no scattered stores.
-template <bool PACK>
-__global__ __launch_bounds__(kCountBlock) void k_count_chunk(CountArgs c) {
-  constexpr int U = kChunk / kCountBlock;
-  __shared__ uint32_t s_ent[kChunk];   // region entries, bucket-sorted; then ids by position
-  __shared__ uint32_t s_pb[kChunk];    // chunk position | bucket << 14 of each sorted entry
-  __shared__ uint32_t s_ch[kSmallNb + 1], s_co[kSmallNb + 1];
-  __shared__ uint32_t s_w[kCountBlock / 64];
-  static_assert(kChunk == kK3Gran && kChunk <= (1u << 14) && kSmallNb < (1u << 18), "layout");
+template <bool PACK, int BS>
+__global__ __launch_bounds__(BS) void k_count_chunk(CountArgs c) {
+  constexpr int U = 16, CH = U * BS;  // records per chunk (c.chunk)
+  __shared__ uint32_t s_ent[CH];   // region entries, bucket-sorted; then ids by position
+  __shared__ uint32_t s_pb[CH];    // chunk position | bucket << 14 of each sorted entry
+  __shared__ uint32_t s_ch[kChunkMaxNb + 1], s_co[kChunkMaxNb + 1];
+  __shared__ uint32_t s_w[BS / 64];
+  static_assert(CH <= (1 << 14) && kChunkMaxNb < BS && kChunkMaxNb < (1u << 18), "layout");
   const uint64_t nflows = c.batch->flow_total;
-  if (count_mode(c, nflows) != 1 || !chunk_scatter(c, nflows)) return;
+  if (count_mode(c, nflows) != 1 || !chunk_scatter(c, nflows) || c.chunk != (uint32_t)CH) return;
+  constexpr uint32_t kCountBlock = BS;  // (the loops below are per workgroup thread)
+  constexpr uint32_t kChunk = CH;
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);  // spare bucket: nb
   const uint64_t n_acc = c.batch->n_acc;
@@ -1659,7 +1662,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count_chunk(CountArgs c) {
     for (int h = 0; h < 2; ++h) {  // two halves of U / 2 loads (register pressure)
       constexpr int H = U / 2;
       uint32_t cl[H], len[H];
-      load_acc<H, PACK>(c, base + (uint64_t)h * H * kCountBlock + tid, base, hi, cl, len);
+      load_acc<H, PACK, BS>(c, base + (uint64_t)h * H * kCountBlock + tid, base, hi, cl, len);
 #pragma unroll
       for (int k = 0; k < H; ++k) {
         const bool big = len[k] >= kRegLenEsc;
@@ -1688,9 +1691,9 @@ __global__ __launch_bounds__(kCountBlock) void k_count_chunk(CountArgs c) {
     __syncthreads();
     {
       uint32_t tot;
-      const uint32_t off = block1024_excl_scan(tid <= nb ? s_ch[tid] : 0u, s_w, tot);
+      const uint32_t off = block1024_excl_scan<BS>(tid <= nb ? s_ch[tid] : 0u, s_w, tot);
       if (tid <= nb) s_co[tid] = off;
-      if (tid <= nb) c.coffs[q * (kSmallNb + 1) + tid] = off;  // [nb] = end of the real buckets
+      if (tid <= nb) c.coffs[q * (kChunkMaxNb + 1) + tid] = off;  // [nb] = end of the real buckets
     }
     __syncthreads();
 #pragma unroll
@@ -1749,10 +1752,10 @@ __global__ __launch_bounds__(kCountBlock) void k_count_bucket(CountArgs c, uint3
   const uint64_t n_acc = c.batch->n_acc;
   // segments: the two-pass scatter's g1 blocks, or k_count_chunk's chunks
   const bool chunked = chunk_scatter(c, nflows);
-  const uint64_t per = chunked ? (uint64_t)kChunk : count_per(n_acc, g1);
-  const uint64_t G = chunked ? (n_acc + kChunk - 1) / kChunk : g1;
+  const uint64_t per = chunked ? (uint64_t)c.chunk : count_per(n_acc, g1);
+  const uint64_t G = chunked ? (n_acc + c.chunk - 1) / c.chunk : g1;
   const uint32_t* obase = chunked ? c.coffs : c.offs;
-  const uint64_t ostride = chunked ? kSmallNb + 1 : c.nb_max + 1;
+  const uint64_t ostride = chunked ? kChunkMaxNb + 1 : c.nb_max + 1;
   constexpr uint32_t kWaves = kCountBlock / 64;
   for (uint64_t q = s + S * wave; q < G; q += S * kWaves) {
     const uint64_t lo_q = q * per;
@@ -2542,10 +2545,14 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
     // (each of the three returns at once unless the batch's bucket count is its own)
     if (c.pack_bits) hipLaunchKernelGGL((k_count_scatter_staged<4, true>), gs, dim3(kCountBlock), 0, s, c);
     else hipLaunchKernelGGL((k_count_scatter_staged<4, false>), gs, dim3(kCountBlock), 0, s, c);
-    if (c.coffs) {  // 132 KiB of LDS: one workgroup per CU (g1s is up to two per CU)
+    if (c.coffs && c.chunk == 16u * 1024u) {  // 132 KiB of LDS: one workgroup per CU
       const dim3 gc((g1s + 1) / 2);
-      if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk<true>), gc, dim3(kCountBlock), 0, s, c);
-      else hipLaunchKernelGGL((k_count_chunk<false>), gc, dim3(kCountBlock), 0, s, c);
+      if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk<true, 1024>), gc, dim3(1024), 0, s, c);
+      else hipLaunchKernelGGL((k_count_chunk<false, 1024>), gc, dim3(1024), 0, s, c);
+    } else if (c.coffs) {  // 8192-record chunks, 68 KiB: two workgroups per CU
+      const dim3 gc(g1s);
+      if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk<true, 512>), gc, dim3(512), 0, s, c);
+      else hipLaunchKernelGGL((k_count_chunk<false, 512>), gc, dim3(512), 0, s, c);
     }
     hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1s);
   }

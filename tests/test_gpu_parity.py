@@ -580,12 +580,13 @@ def _concat(a, b):
                  np.concatenate([a.caplen, b.caplen]), np.concatenate([a.ts_ns, b.ts_ns]))
 
 
-@pytest.mark.parametrize("variant", ["0", "91"])
+@pytest.mark.parametrize("variant", ["0", "91", "92"])
 @pytest.mark.parametrize("flows", [40_000, 150_000])
 def test_k3_chunked_scatter(gpu, oracle, variant, flows, monkeypatch):
     """K3 mode 1's single-pass chunked scatter (k_count_chunk: chunks of 16384
-    records bucket-sorted in LDS, ids gathered bucket by bucket, region runs per
-    chunk) and the two-pass scatter it replaced (TCBEE_K3ABL=91), bit-exact vs the
+    records — 8192 with TCBEE_K3ABL=92 — bucket-sorted in LDS, ids gathered bucket
+    by bucket, region runs per chunk) and the two-pass scatter it replaced
+    (TCBEE_K3ABL=91), bit-exact vs the
     oracle: a ragged last chunk, caplens past the 20-bit region field and the
     packed K1 -> K3 field, a single-flow stretch (every wave on one bucket), two
     batches (claims of batch 1 looked up again in batch 2)."""
