@@ -1652,11 +1652,17 @@ __global__ __launch_bounds__(BS) void k_count_chunk(CountArgs c) {
   const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);  // spare bucket: nb
   const uint64_t n_acc = c.batch->n_acc;
   const uint64_t nchunks = (n_acc + kChunk - 1) / kChunk;
+  // Barriers per chunk: rank | scan (2) | offsets | placed | read | ids. The counts
+  // are zeroed right after the scan has read them (before three more barriers), so a
+  // workgroup's waves may run into the next chunk's loads and ranks while others
+  // still store this chunk's ids (nothing those touch is reused before the next
+  // rank barrier)
+  for (uint32_t b = tid; b <= nb; b += kCountBlock) s_ch[b] = 0;
+  __syncthreads();
   for (uint64_t q = blockIdx.x; q < nchunks; q += gridDim.x) {
     const uint64_t base = q * kChunk;
     const uint64_t hi = base + kChunk < n_acc ? base + kChunk : n_acc;
     const uint32_t nval = (uint32_t)(hi - base);
-    for (uint32_t b = tid; b <= nb; b += kCountBlock) s_ch[b] = 0;
     uint32_t ent[U], bk[U], lp[U];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {  // two halves of U / 2 loads (register pressure)
@@ -1672,7 +1678,6 @@ __global__ __launch_bounds__(BS) void k_count_chunk(CountArgs c) {
           atomicAdd((unsigned long long*)&c.cnt[2ull * c.cmap[cl[k]] + 1], (unsigned long long)len[k]);
       }
     }
-    __syncthreads();
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const bool valid = (uint32_t)k * kCountBlock + tid < nval;
@@ -1694,6 +1699,7 @@ __global__ __launch_bounds__(BS) void k_count_chunk(CountArgs c) {
       const uint32_t off = block1024_excl_scan<BS>(tid <= nb ? s_ch[tid] : 0u, s_w, tot);
       if (tid <= nb) s_co[tid] = off;
       if (tid <= nb) c.coffs[q * (kChunkMaxNb + 1) + tid] = off;  // [nb] = end of the real buckets
+      if (tid <= nb) s_ch[tid] = 0;  // read by the scan only: zero for the next chunk
     }
     __syncthreads();
 #pragma unroll
@@ -1731,7 +1737,6 @@ __global__ __launch_bounds__(BS) void k_count_chunk(CountArgs c) {
         if (p < hi && p < c.out_cap) __builtin_nontemporal_store(s_ent[(uint32_t)k * kCountBlock + tid], &c.out_id[p]);
       }
     }
-    __syncthreads();  // before the next chunk reuses s_ch / s_ent
   }
 }
 
