@@ -1659,11 +1659,41 @@ __global__ __launch_bounds__(BS) void k_count_chunk(CountArgs c) {
   // rank barrier)
   for (uint32_t b = tid; b <= nb; b += kCountBlock) s_ch[b] = 0;
   __syncthreads();
+  // packed K1 -> K3 words: the next chunk's words are loaded while this chunk's
+  // sorted entries are read and its ids stored (one workgroup per CU: nothing else
+  // hides that load)
+  uint32_t nxt[PACK ? U : 1];
+  auto prefetch = [&](uint64_t qn) {
+    if constexpr (PACK) {
+      const uint64_t b0 = qn * kChunk;
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint64_t p = b0 + (uint64_t)k * kCountBlock + tid;
+        nxt[k] = qn < nchunks && p < n_acc ? __builtin_nontemporal_load(&c.acc_flow[p]) : 0xFFFFFFFFu;
+      }
+    }
+  };
+  prefetch(blockIdx.x);
+  const uint32_t lmax = 0xFFFFFFFFu >> c.pack_bits;
   for (uint64_t q = blockIdx.x; q < nchunks; q += gridDim.x) {
     const uint64_t base = q * kChunk;
     const uint64_t hi = base + kChunk < n_acc ? base + kChunk : n_acc;
     const uint32_t nval = (uint32_t)(hi - base);
     uint32_t ent[U], bk[U], lp[U];
+    if constexpr (PACK) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint32_t v = nxt[k];
+        const uint32_t cl = v == 0xFFFFFFFFu ? v : (v & ((1u << c.pack_bits) - 1u));
+        uint32_t len = v == 0xFFFFFFFFu ? 0u : v >> c.pack_bits;
+        if (len == lmax) len = c.acc_len[base + (uint64_t)k * kCountBlock + tid];  // saturated
+        const bool big = len >= kRegLenEsc;
+        bk[k] = cl != 0xFFFFFFFFu ? (cl >> kBucketBits) : nb;
+        ent[k] = (cl & (kBucket - 1u)) | ((big ? 0u : len) << kBucketBits);
+        if (big && cl != 0xFFFFFFFFu)
+          atomicAdd((unsigned long long*)&c.cnt[2ull * c.cmap[cl] + 1], (unsigned long long)len);
+      }
+    } else
 #pragma unroll
     for (int h = 0; h < 2; ++h) {  // two halves of U / 2 loads (register pressure)
       constexpr int H = U / 2;
@@ -1711,6 +1741,7 @@ __global__ __launch_bounds__(BS) void k_count_chunk(CountArgs c) {
       s_pb[idx] = pos | (bk[k] << 14);
     }
     __syncthreads();
+    prefetch(q + gridDim.x);
     uint32_t id[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
