@@ -2564,7 +2564,10 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
     default: KC(8, 0); break;
   }
 #undef KC
-  if (g2) {
+  // the two-pass scatter only where the chunked one may not cover a batch (tables
+  // of >= kChunkMaxNb buckets, or the A/B hook): no empty launches otherwise
+  const bool two_pass = !c.coffs || c.chunk_off || c.nb_max >= kChunkMaxNb;
+  if (g2 && two_pass) {
     const dim3 gs(g1s);
     switch (k3v) {  // 64 + SABL: timing-only scatter ablations
       case 65: hipLaunchKernelGGL((k_count_scatter<8, false, 1>), gs, dim3(kCountBlock), 0, s, c); break;
@@ -2581,12 +2584,14 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
     // (each of the three returns at once unless the batch's bucket count is its own)
     if (c.pack_bits) hipLaunchKernelGGL((k_count_scatter_staged<4, true>), gs, dim3(kCountBlock), 0, s, c);
     else hipLaunchKernelGGL((k_count_scatter_staged<4, false>), gs, dim3(kCountBlock), 0, s, c);
+  }
+  if (g2) {
     if (c.coffs && c.chunk == 16u * 1024u) {  // 132 KiB of LDS: one workgroup per CU
       const dim3 gc((g1s + 1) / 2);
       if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk<true, 1024>), gc, dim3(1024), 0, s, c);
       else hipLaunchKernelGGL((k_count_chunk<false, 1024>), gc, dim3(1024), 0, s, c);
     } else if (c.coffs) {  // 8192-record chunks, 68 KiB: two workgroups per CU
-      const dim3 gc(g1s);
+      const dim3 gc(g1s ? g1s : 1);
       if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk<true, 512>), gc, dim3(512), 0, s, c);
       else hipLaunchKernelGGL((k_count_chunk<false, 512>), gc, dim3(512), 0, s, c);
     }
