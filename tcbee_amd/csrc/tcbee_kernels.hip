@@ -1822,7 +1822,8 @@ __global__ __launch_bounds__(kCountBlock) void k_count_bucket(CountArgs c, uint3
 
 // K3 reduce: mode 0 sums the g1 packed partial rows per dense id; mode 1 sums
 // the S partial rows per claim and maps claims to ids. cnt is by dense id.
-__global__ void k_count_reduce(CountArgs c, uint32_t g1, uint32_t g2) {
+constexpr int kReduceWaves = 16;  // k_count_reduce: 1024-thread blocks
+__global__ __launch_bounds__(64 * kReduceWaves) void k_count_reduce(CountArgs c, uint32_t g1, uint32_t g2) {
   const uint64_t nflows = c.batch->flow_total;
   const int mode = count_mode(c, nflows);
   const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -1848,30 +1849,48 @@ __global__ void k_count_reduce(CountArgs c, uint32_t g1, uint32_t g2) {
       }
     }
   } else if (mode == 0) {
-    for (uint64_t f = t0; f < nflows; f += stride) {
-      // 8 independent rows per step: the loads of a thread are in flight together
+    // a block takes 64 consecutive claims (lane = claim) and its waves split the
+    // g1 rows (each row read as one 512-B run, 8 rows in flight per lane); the
+    // waves' sums meet in LDS — a thread per claim walking all g1 rows was a
+    // dependent chain of g1 / 8 load rounds (config 3: 15 us)
+    __shared__ uint64_t s_red[2][kReduceWaves][64];
+    const uint32_t nw = blockDim.x >> 6, w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    for (uint64_t fg = blockIdx.x; fg * 64 < nflows; fg += gridDim.x) {
+      const uint64_t f = fg * 64 + lane;
       uint64_t pk = 0, by = 0;
-      uint32_t b = 0;
-      for (; b + 8 <= g1; b += 8) {
-        uint64_t v[8];
+      if (f < nflows) {
+        uint32_t b = w;
+        for (; b + 7 * nw < g1; b += 8 * nw) {
+          uint64_t v[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = c.part[(uint64_t)(b + k) * kCountBins + f];
+          for (int k = 0; k < 8; ++k) v[k] = c.part[(uint64_t)(b + k * nw) * kCountBins + f];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          pk += v[k] >> kBinPkShift;
-          by += v[k] & kBinByMask;
+          for (int k = 0; k < 8; ++k) {
+            pk += v[k] >> kBinPkShift;
+            by += v[k] & kBinByMask;
+          }
+        }
+        for (; b < g1; b += nw) {
+          const uint64_t v = c.part[(uint64_t)b * kCountBins + f];
+          pk += v >> kBinPkShift;
+          by += v & kBinByMask;
         }
       }
-      for (; b < g1; ++b) {
-        const uint64_t v = c.part[(uint64_t)b * kCountBins + f];
-        pk += v >> kBinPkShift;
-        by += v & kBinByMask;
+      s_red[0][w][lane] = pk;
+      s_red[1][w][lane] = by;
+      __syncthreads();
+      if (w == 0 && f < nflows) {
+        for (uint32_t x = 1; x < nw; ++x) {
+          pk += s_red[0][x][lane];
+          by += s_red[1][x][lane];
+        }
+        if (pk) {  // rows are by claim; counters by local dense id
+          const uint32_t id = c.cmap[f];
+          c.cnt[2ull * id] += pk;
+          c.cnt[2ull * id + 1] += by;
+        }
       }
-      if (pk) {  // rows are by claim; counters by local dense id
-        const uint32_t id = c.cmap[f];
-        c.cnt[2ull * id] += pk;
-        c.cnt[2ull * id + 1] += by;
-      }
+      __syncthreads();
     }
   } else if (mode == 3) {
     const uint32_t G = 8u * range_groups_per_x(c, nflows);
@@ -2598,8 +2617,9 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
     hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1s);
   }
   // mode 0 needs kCountBins threads; mode 1 up to nb_max * kBucket (grid-stride)
-  const unsigned gr = (g2 || c.range_ok) ? 1024u : (unsigned)(kCountBins / 256);
-  hipLaunchKernelGGL(k_count_reduce, dim3(gr), dim3(256), 0, s, c, g1, g2);  // g1: mode-0 rows
+  // (1024-thread blocks: mode 0 takes 64 claims per block, its 16 waves split the rows)
+  const unsigned gr = (g2 || c.range_ok) ? 256u : (unsigned)(kCountBins / 256);
+  hipLaunchKernelGGL(k_count_reduce, dim3(gr), dim3(64 * kReduceWaves), 0, s, c, g1, g2);  // g1: mode-0 rows
   return hipGetLastError();
 }
 
