@@ -36,7 +36,7 @@ struct PersistState {
   uint64_t flow_count;  // flows with ids
   uint32_t status;
   uint32_t k3_mode;     // diagnostic: K3 mode of the last batch + 1 (0: none yet)
-  uint64_t pad1;
+  uint64_t blocks_done; // k_assign's finished blocks (the last one resets it)
 };
 
 // Zeroed before every batch (one 32-B memset).

@@ -1098,13 +1098,22 @@ __global__ void k_assign(RankArgs r) {
     if (r.update_persist) r.tab.cnt[2 * id] = r.tab.cnt[2 * id + 1] = 0;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) r.batch->flow_total = fbase + n_new;
+  if (r.update_persist) {
+    // the batch is classified: the last block to finish advances the context's
+    // record base and flow count (was its own one-thread launch). Every block read
+    // both above, before its count, so none reads them after the update
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint64_t done = atomicAdd((unsigned long long*)&r.persist->blocks_done, 1ull);
+      if (done == gridDim.x - 1) {
+        r.persist->rec_base = base + r.batch->n_acc;
+        r.persist->flow_count = fbase + n_new;
+        r.persist->blocks_done = 0;
+      }
+    }
+  }
 }
 
-// after the multi-kernel rank: advance the context's record base / flow count
-__global__ void k_rank_done(RankArgs r) {
-  r.persist->rec_base += r.batch->n_acc;
-  r.persist->flow_count = r.batch->flow_total;
-}
 
 // K3: per accepted frame, claim index -> dense id (written for records p <
 // out_cap) and pkts/bytes per flow. Three modes, chosen on the device from the
@@ -2560,7 +2569,7 @@ hipError_t launch_rank(const RankArgs& r, hipStream_t s) {
                      0, s, r);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, r);
   hipLaunchKernelGGL(k_assign, dim3(1024), dim3(kBlock), 0, s, r);
-  if (r.update_persist) hipLaunchKernelGGL(k_rank_done, dim3(1), dim3(1), 0, s, r);
+  // (k_assign's last block advances the record base / flow count)
   return hipGetLastError();
 }
 
