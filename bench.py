@@ -289,16 +289,19 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
             check["exchange_entries_per_rank"] = xcap
     if flowhash:
         check["frames_local"] = n
-        if rank == 0:
-            check.update(validate_shard(torch, last["rec"], last["hash"], last["id"], gidx, n,
-                                        sizes, kind, n_flows, seed, nrec, global_ids=multi))
+        # every rank checks its own shard (global ids included) against the oracle
+        check.update(validate_shard(torch, last["rec"], last["hash"], last["id"], gidx, n,
+                                    sizes, kind, n_flows, seed, nrec, global_ids=multi))
     elif rank == 0 and full_check and not multi:
         check.update(validate_full(torch, last["rec"], last["hash"], last["id"], n, sizes, kind,
                                    n_flows, seed, nrec, flows,
                                    table_mult=count[0] if warm else 1))
-    elif rank == 0:
+    else:
         check.update(validate_sample(torch, last["rec"], last["hash"], n, sizes, kind, n_flows,
                                      seed, first, nrec))
+    if multi:
+        check.update(all_ranks_check(torch, dist, check, status, n, n_global if flowhash
+                                     else world * n, flows, last["ctr"]))
     if ox is not None:
         ox.owner.close()
     p.close()
@@ -307,6 +310,29 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     del d_arena, slots
     torch.cuda.empty_cache()
     return elapsed, k1_ms / max(k1_launches, 1), nrec, check, n
+
+
+def all_ranks_check(torch, dist, check, status, n_local, n_global, flows, ctr):
+    """One verdict for the whole job (collective): every rank's own oracle check and
+    context status, MIN-reduced into all_ranks_bit_exact; the global table and
+    counters against the global frame count (every synthetic frame is accepted);
+    the flow-hash shard imbalance (max / mean local frames), which bounds weak-scaling
+    efficiency."""
+    ok = bool(check.get("sample_bit_exact", check.get("full_bit_exact", False))) and status == 0
+    v = torch.tensor([int(ok)], dtype=torch.int64, device="cuda")
+    dist.all_reduce(v, op=dist.ReduceOp.MIN)
+    mx = torch.tensor([n_local], dtype=torch.int64, device="cuda")
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    sm = torch.tensor([n_local], dtype=torch.int64, device="cuda")
+    dist.all_reduce(sm)
+    world = dist.get_world_size()
+    mean = int(sm.item()) / world
+    return {"all_ranks_bit_exact": bool(v.item()), "ranks_checked": world,
+            "frames_local_max": int(mx.item()), "frames_local_mean": round(mean, 1),
+            "shard_imbalance": round(int(mx.item()) / mean, 4) if mean else None,
+            "global_frames_ok": int(sm.item()) == n_global,
+            "global_pkts_ok": int(flows["pkts"].sum()) == n_global,
+            "global_ingress_ok": int(ctr[0].item()) == n_global}
 
 
 def validate_shard(torch, d_rec, d_hash, d_id, gidx, n, sizes, kind, n_flows, seed, nrec,
@@ -593,13 +619,20 @@ def pmc_traffic(args, k1_ms):
             "traffic_GBs": round(t / (k1_ms * 1e-3) / 1e9, 1)}
 
 
+def max_over_ranks(torch, dist, x: float) -> float:
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=100_000_000, help="frames per GPU")
-    ap.add_argument("--sizes", default="imix", choices=["imix", "64"])
+    ap.add_argument("--sizes", default="imix", choices=["imix", "64", "imix6"],
+                    help="imix6: the IPv6/TCP trace (78/576/1500 B) as the main leg")
     ap.add_argument("--flows", type=int, default=10_000)
     ap.add_argument("--seed", type=int, default=0x7CBEE)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -618,6 +651,11 @@ def main():
                          "(its frames and flows; no exchange) to measure one GPU's share")
     ap.add_argument("--sample-check", action="store_true",
                     help="N=1: check 2 x 200k records instead of every record + the table")
+    ap.add_argument("--c4-frames", type=int, default=125_000_000,
+                    help="N>1: frames per GPU of the config-4 leg (1M flows, flow-hash "
+                         "shards, FlowHashExchange); 125M = BASELINE.json's 1B at N=8. "
+                         "Smaller only to rehearse N ranks on one GPU")
+    ap.add_argument("--c4-steps", type=int, default=5)
     args = ap.parse_args()
     if args.config4:
         args.frames, args.flows, args.sizes = 125_000_000, 1_000_000, "imix"
@@ -651,7 +689,7 @@ def main():
     # default-stream handle (0) would put the parse/merge on streams the collectives
     # and the remap do not wait for.
     torch.cuda.set_stream(torch.cuda.Stream())
-    kind = 1 if args.flows > 1 else 0
+    kind = 3 if args.sizes == "imix6" else (1 if args.flows > 1 else 0)
 
     elapsed, k1_ms, nrec, check, n_local = run_device(
         torch, dist, rank, world, args.frames, args.sizes, kind, args.flows, args.steps,
@@ -659,9 +697,26 @@ def main():
         full_check=not args.sample_check, flowhash=args.shard == "flowhash",
         vworld=args.virtual_world)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(torch, dist, elapsed)
+    c4 = None
+    if world > 1 and not args.no_extra and not args.config4:
+        # north_star's config 4 at N GPUs (BASELINE.json configs[3]): 1M flows,
+        # --c4-frames per GPU (1B frames in all at N=8), flow-hash shards, global ids
+        # from the FlowHashExchange over RCCL, counters all-reduced; every rank checks
+        # its shard against the oracle (collective, all ranks take part)
+        log(f"rank {rank}: config-4 leg ({args.c4_frames} frames per GPU, 1M flows)")
+        c_el, c_k1, c_n, c_chk, c_local = run_device(
+            torch, dist, rank, world, args.c4_frames, "imix", 1, 1_000_000, args.c4_steps, 1,
+            args.seed, multi=True, flowhash=True)
+        c_el = max_over_ranks(torch, dist, c_el)
+        c4 = {"workload": "config4: IMIX 64/576/1500 7:4:1 IPv4/TCP, 1000000 flows, "
+                          "flow-hash shards, FlowHashExchange",
+              "frames_global": args.c4_frames * world, "frames_per_gpu": args.c4_frames,
+              "flows": 1_000_000, "steps": args.c4_steps,
+              "mpkts": round(args.c4_frames * world * args.c4_steps / c_el / 1e6, 1),
+              "ms_per_step": round(c_el / args.c4_steps * 1e3, 4),
+              "k1_ms_rank0": round(c_k1, 4), "exchange_ms_rank0": c_chk.get("exchange_ms"),
+              "check": c_chk}
     ms_per_step = elapsed / args.steps * 1e3
     total_frames = args.frames * world * args.steps
     value = total_frames / elapsed / 1e6
@@ -669,7 +724,7 @@ def main():
     out = None
     if rank == 0:
         # roofline of the dominant kernel (K1 k_parse), algorithmic bytes per launch
-        hdr = V4_HDR_BYTES  # synthetic frames are IPv4/TCP
+        hdr = 74 if args.sizes == "imix6" else V4_HDR_BYTES  # IPv6 / IPv4 TCP headers
         alg_bytes = n_local * (IDX_BYTES + hdr) + nrec * OUT_BYTES
         achieved = alg_bytes / (k1_ms * 1e-3) / 1e9
         out = {
@@ -677,10 +732,11 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": (("config4: " if args.config4 else "config3: ")
-                                    + "IMIX 64/576/1500 7:4:1 IPv4/TCP, "
-                                    f"{args.flows} flows" if args.sizes == "imix"
-                                    else f"64B IPv4/TCP, {args.flows} flow(s)"),
+            "config": {"workload": {
+                "imix": ("config4: " if args.config4 else "config3: ")
+                + f"IMIX 64/576/1500 7:4:1 IPv4/TCP, {args.flows} flows",
+                "imix6": f"config3 over IPv6/TCP: IMIX 78/576/1500 7:4:1, {args.flows} flows",
+                "64": f"64B IPv4/TCP, {args.flows} flow(s)"}[args.sizes],
                        "shard": args.shard + (f" (rank 0 of {args.virtual_world})"
                                               if args.virtual_world and world == 1 else ""),
                        "frames_per_gpu": args.frames, "flows": args.flows,
@@ -693,6 +749,10 @@ def main():
                          "alg_bytes_per_frame": IDX_BYTES + hdr + OUT_BYTES},
             "check": check,
         }
+        if dist is not None:
+            out["dist"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size()}
+        if c4 is not None:
+            out["config4_flowhash"] = c4
         if not args.no_extra and world == 1 and not args.config4:
             e_el, e_k1, e_n, e_chk, _ = run_device(torch, None, 0, 1, 1_000_000, "64", 0, 1,
                                                 max(args.steps, 20), args.warmup, args.seed,

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define TCBEE_ABI_VERSION 2
+#define TCBEE_ABI_VERSION 3  /* 3: owner meta world+2 words, tcbee_status_raise_device */
 
 /* ---- record / key layout constants (DESIGN.md "Data layout") ------------ */
 #define TCBEE_RECORD_BYTES   74  /* tcp_packet.rs:42 ENTRY_SIZE            */
@@ -172,8 +172,11 @@ typedef struct tcbee_parse_ex {
     /* TCBEE_EX_DEFER_IDS: records, hashes and the flow table (with local dense ids)
      * are produced; the per-record flow ids, pkts/bytes, counters and out_n are
      * written by tcbee_parse_finish_device, which must come before any other call
-     * on the context except tcbee_flow_first_frames_device (the exchange's input;
-     * tcbee_flow_export_global_device also places flows then, without counts). */
+     * on the context except the exchanges' calls, which read only the table's keys,
+     * first_seen and local ids: tcbee_flow_first_frames_device (the flow-hash
+     * exchange's input), tcbee_owner_bucket_device (the owner exchange's input),
+     * tcbee_status_raise_device, and tcbee_flow_export_global_device (it places
+     * flows then, without counts). */
     uint32_t  flags;
     uint32_t  reserved32;    /* zero */
     /* TCBEE_EX_ASYNC_IDS: K3 — the per-record flow ids, pkts/bytes, counters and
@@ -282,9 +285,15 @@ int tcbee_global_ids_device(const uint64_t* all_first_frame_dev, const uint64_t*
  *    seg_cap entries (segment o at ent_dev + o*seg_cap: key, pkts/bytes 0,
  *    first_seen local), lid_dev = local id of each entry, meta_dev[0..world) =
  *    entries per owner (the ones past seg_cap, and flows whose local id is not
- *    below map_cap — the local -> global map's size — are dropped and the
- *    context's status reports TCBEE_ESHARD), meta_dev[world] = the context's records;
+ *    below map_cap — the local -> global map's size — are dropped: a map_cap drop
+ *    takes no segment slot; the context's status reports TCBEE_ESHARD),
+ *    meta_dev[world] = the context's records, meta_dev[world + 1] = entries dropped
+ *    (ABI 3: meta_dev holds world + 2 words);
  *  -> all-gather of meta, all-to-all of the segments (rank r's segment o to o);
+ *  tcbee_status_raise_device(ctx, all_meta + world + 1, world, world + 2): a peer's
+ *    drops make every rank's global ids unreliable, so every rank's context then
+ *    reports TCBEE_ESHARD as well (generally: ESHARD if any v_dev[i * stride],
+ *    i < n, is non-zero);
  *  -> the owner merges what it received with tcbee_flow_merge_device (segment r
  *    = rank r's entries, seg_meta {count, records of rank r}: first_seen rebased
  *    to the global record stream) on a second context;
@@ -300,6 +309,8 @@ int tcbee_global_ids_device(const uint64_t* all_first_frame_dev, const uint64_t*
  * HIP's null stream, as tcbee_remap_ids_device does: pass the caller's stream. */
 int tcbee_owner_bucket_device(tcbee_ctx* ctx, uint32_t world, uint64_t seg_cap, uint64_t map_cap,
                               tcbee_flow_entry* ent_dev, uint32_t* lid_dev, uint64_t* meta_dev,
+                              void* stream);
+int tcbee_status_raise_device(tcbee_ctx* ctx, const uint64_t* v_dev, uint64_t n, uint64_t stride,
                               void* stream);
 int tcbee_flow_first_seen_device(tcbee_ctx* ctx, uint64_t* out_dev, uint64_t cap, uint64_t* n_dev,
                                  void* stream);

@@ -114,6 +114,8 @@ _SIGS = {
                                                  C.c_uint64, C.c_uint64, C.c_void_p]),
     "tcbee_owner_bucket_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64,
                                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "tcbee_status_raise_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
+                                            C.c_void_p]),
     "tcbee_flow_first_seen_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
                                                C.c_void_p]),
     "tcbee_owner_return_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64,

@@ -639,7 +639,7 @@ int tcbee_owner_bucket_device(tcbee_ctx* c, uint32_t world, uint64_t seg_cap, ui
   TRY_HIP(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if (int rc = apply_pending_reset(c, s)) return rc;
-  TRY_HIP(hipMemsetAsync(meta_dev, 0, (world + 1ull) * sizeof(uint64_t), s));
+  TRY_HIP(hipMemsetAsync(meta_dev, 0, (world + 2ull) * sizeof(uint64_t), s));
   OwnerArgs a{};
   a.tab = c->tab;
   a.persist = c->d_persist;
@@ -651,6 +651,16 @@ int tcbee_owner_bucket_device(tcbee_ctx* c, uint32_t world, uint64_t seg_cap, ui
   a.meta = meta_dev;
   a.status = &c->d_persist->status;
   TRY_HIP(launch_owner_bucket(a, s));
+  return TCBEE_OK;
+}
+
+int tcbee_status_raise_device(tcbee_ctx* c, const uint64_t* v_dev, uint64_t n, uint64_t stride,
+                              void* stream) {
+  if (!c || (n && !v_dev) || (n > 1 && !stride)) return TCBEE_EINVAL;
+  if (!n) return TCBEE_OK;
+  TRY_HIP(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  TRY_HIP(launch_status_raise(v_dev, n, stride, &c->d_persist->status, s));
   return TCBEE_OK;
 }
 

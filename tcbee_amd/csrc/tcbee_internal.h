@@ -36,7 +36,11 @@ struct PersistState {
   uint64_t flow_count;  // flows with ids
   uint32_t status;
   uint32_t k3_mode;     // diagnostic: K3 mode of the last batch + 1 (0: none yet)
-  uint64_t blocks_done; // k_assign's finished blocks (the last one resets it)
+  // rec_base / flow_count as they were before this batch's rank step: k_scan_blocks
+  // (one block, before k_assign) stages them here and advances the two above, so
+  // k_assign reads the old bases without any grid-wide completion count
+  uint64_t rank_base;
+  uint64_t rank_fbase;
 };
 
 // Zeroed before every batch (one 32-B memset).
@@ -199,12 +203,16 @@ struct OwnerArgs {
   uint64_t seg_cap;
   uint64_t* ent;        // [world][seg_cap] tcbee_flow_entry (u64[8])
   uint32_t* lid;        // [world][seg_cap] local id of each entry
-  uint64_t* meta;       // [world + 1]: entries per owner (zeroed first; may pass
-                        // seg_cap: the rest are dropped, TCBEE_ESHARD), records
+  uint64_t* meta;       // [world + 2]: entries per owner (zeroed first; may pass
+                        // seg_cap: the rest are dropped, TCBEE_ESHARD), records,
+                        // entries dropped (seg_cap or map_cap)
   uint64_t map_cap;     // local ids past it have no place in the id map: ESHARD
   uint32_t* status;     // persist->status of the context (ESHARD on overflow)
 };
 hipError_t launch_owner_bucket(const OwnerArgs& a, hipStream_t s);
+// *status |= kStShard if any v[i * stride] != 0, i < n (one block)
+hipError_t launch_status_raise(const uint64_t* v, uint64_t n, uint64_t stride, uint32_t* status,
+                               hipStream_t s);
 // out[id] = first_seen of flow id (dense-id order: ascending), n_out = {flows, 0}
 hipError_t launch_first_seen(FlowTable t, const PersistState* p, uint64_t* out, uint64_t cap,
                              uint64_t* n_out, hipStream_t s);

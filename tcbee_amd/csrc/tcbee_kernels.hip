@@ -1066,6 +1066,21 @@ __global__ __launch_bounds__(kBlock) void k_scan_words(RankArgs r) {
 
 __global__ __launch_bounds__(kBlock) void k_scan_blocks(RankArgs r) {
   __shared__ uint32_t s_tmp[4];
+  if (threadIdx.x == 0) {
+    // k_assign (next launch) reads the bases staged here; the batch is classified
+    // once it runs, so the context's bases advance now (nothing between this
+    // launch and k_assign reads them). Round 2 had k_assign's last block do it:
+    // one same-address device atomic per block cost ~10 us
+    const uint64_t base = r.persist->rec_base, fbase = r.persist->flow_count;
+    const uint64_t n_new = r.batch->n_new;
+    r.persist->rank_base = base;
+    r.persist->rank_fbase = fbase;
+    r.batch->flow_total = fbase + n_new;
+    if (r.update_persist) {
+      r.persist->rec_base = base + r.batch->n_acc;
+      r.persist->flow_count = fbase + n_new;
+    }
+  }
   uint32_t carry = 0;
   const uint64_t nb = (rank_words(r) + kScanWordsPerBlock - 1) / kScanWordsPerBlock;
   for (uint64_t b0 = 0; b0 < nb; b0 += kBlock) {
@@ -1080,9 +1095,11 @@ __global__ __launch_bounds__(kBlock) void k_scan_blocks(RankArgs r) {
 
 __global__ void k_assign(RankArgs r) {
   const uint64_t n_new = r.batch->n_new;
+  // surplus blocks (the grid is fixed: the host does not know n_new) leave at once
+  if (blockIdx.x * (uint64_t)blockDim.x >= n_new) return;
   const uint64_t lim = rank_words(r);
-  const uint64_t base = r.persist->rec_base;
-  const uint64_t fbase = r.persist->flow_count;
+  const uint64_t base = r.persist->rank_base;    // staged by k_scan_blocks
+  const uint64_t fbase = r.persist->rank_fbase;
   for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n_new;
        j += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t s = r.new_list[j];
@@ -1096,21 +1113,6 @@ __global__ void k_assign(RankArgs r) {
     r.tab.meta[8 * s + 7] = id + 1;
     r.tab.cmap[fbase + j] = (uint32_t)id;
     if (r.update_persist) r.tab.cnt[2 * id] = r.tab.cnt[2 * id + 1] = 0;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) r.batch->flow_total = fbase + n_new;
-  if (r.update_persist) {
-    // the batch is classified: the last block to finish advances the context's
-    // record base and flow count (was its own one-thread launch). Every block read
-    // both above, before its count, so none reads them after the update
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint64_t done = atomicAdd((unsigned long long*)&r.persist->blocks_done, 1ull);
-      if (done == gridDim.x - 1) {
-        r.persist->rec_base = base + r.batch->n_acc;
-        r.persist->flow_count = fbase + n_new;
-        r.persist->blocks_done = 0;
-      }
-    }
   }
 }
 
@@ -2158,6 +2160,7 @@ __global__ __launch_bounds__(kBlock) void k_owner_bucket(OwnerArgs a) {
   __syncthreads();
   uint32_t own[kOwnerItems], rank[kOwnerItems];
   const uint64_t s0 = (uint64_t)blockIdx.x * kBlock * kOwnerItems + tid;
+  uint32_t dropped = 0;
 #pragma unroll
   for (int k = 0; k < kOwnerItems; ++k) {
     own[k] = 0xFFFFFFFFu;
@@ -2165,6 +2168,12 @@ __global__ __launch_bounds__(kBlock) void k_owner_bucket(OwnerArgs a) {
     if (s >= nslots) continue;
     const uint64_t* m = a.tab.meta + 8 * s;
     if (m[0] < 2 || m[7] == 0) continue;
+    // a flow whose local id has no place in the id map takes NO segment slot (a
+    // counted but unwritten slot would reach its owner as a phantom flow)
+    if (m[7] - 1 >= a.map_cap) {
+      ++dropped;
+      continue;
+    }
     own[k] = fold32(flow_hash64(m[1], m[2], m[3], m[4], m[5])) % a.world;
     rank[k] = atomicAdd(&s_cnt[own[k]], 1u);
   }
@@ -2174,15 +2183,14 @@ __global__ __launch_bounds__(kBlock) void k_owner_bucket(OwnerArgs a) {
     s_base[tid] = c ? atomicAdd((unsigned long long*)&a.meta[tid], (unsigned long long)c) : 0ull;
   }
   __syncthreads();
-  bool over = false;
 #pragma unroll
   for (int k = 0; k < kOwnerItems; ++k) {
     if (own[k] == 0xFFFFFFFFu) continue;
     const uint64_t pos = s_base[own[k]] + rank[k];
     const uint64_t s = s0 + (uint64_t)k * kBlock;
     const uint64_t* m = a.tab.meta + 8 * s;
-    if (pos >= a.seg_cap || m[7] - 1 >= a.map_cap) {
-      over = true;
+    if (pos >= a.seg_cap) {  // positions [0, seg_cap) of every segment stay dense
+      ++dropped;
       continue;
     }
     const uint64_t e = (uint64_t)own[k] * a.seg_cap + pos;
@@ -2194,7 +2202,22 @@ __global__ __launch_bounds__(kBlock) void k_owner_bucket(OwnerArgs a) {
     out[7] = m[6];  // first_seen, local to this rank's record stream
     a.lid[e] = (uint32_t)(m[7] - 1);
   }
-  if (__any(over) && __lane_id() == 0) atomicOr(a.status, kStShard);
+  // meta[world + 1]: entries this rank dropped. Every rank sees it after the meta
+  // all-gather, so the PEERS of an overflowing rank can flag their ids as wrong too
+  // (tcbee_status_raise_device), not only the rank that dropped them
+  for (int o = 32; o > 0; o >>= 1) dropped += __shfl_xor(dropped, o);
+  if (dropped && __lane_id() == 0) {
+    atomicOr(a.status, kStShard);
+    atomicAdd((unsigned long long*)&a.meta[a.world + 1], (unsigned long long)dropped);
+  }
+}
+
+// status |= kStShard when any v[i * stride] (i < n) is non-zero: a peer's dropped
+// owner entries (OwnerExchange) make this rank's global ids unreliable as well
+__global__ void k_status_raise(const uint64_t* v, uint64_t n, uint64_t stride, uint32_t* status) {
+  bool any = false;
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) any |= v[i * stride] != 0;
+  if (__any(any) && __lane_id() == 0) atomicOr(status, kStShard);
 }
 
 __global__ void k_first_seen(FlowTable t, const PersistState* p, uint64_t* out, uint64_t cap,
@@ -2569,7 +2592,8 @@ hipError_t launch_rank(const RankArgs& r, hipStream_t s) {
                      0, s, r);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, r);
   hipLaunchKernelGGL(k_assign, dim3(1024), dim3(kBlock), 0, s, r);
-  // (k_assign's last block advances the record base / flow count)
+  // (k_scan_blocks advances the record base / flow count; k_assign reads the staged
+  //  old ones, and its blocks past n_new return before touching anything)
   return hipGetLastError();
 }
 
@@ -2666,6 +2690,12 @@ hipError_t launch_owner_bucket(const OwnerArgs& a, hipStream_t s) {
   const uint64_t per = (uint64_t)kBlock * kOwnerItems;
   const uint64_t nb = (a.tab.mask + 1 + per - 1) / per;
   hipLaunchKernelGGL(k_owner_bucket, dim3((unsigned)nb), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_status_raise(const uint64_t* v, uint64_t n, uint64_t stride, uint32_t* status,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(k_status_raise, dim3(1), dim3(kBlock), 0, s, v, n, stride, status);
   return hipGetLastError();
 }
 

@@ -334,8 +334,9 @@ class OwnerExchange:
         self.send = torch.zeros((W * seg_cap, ENTRY_WORDS), dtype=torch.int64, device=dev)
         self.recv = torch.zeros_like(self.send)
         self.lid = torch.zeros(W * seg_cap, dtype=torch.int32, device=dev)
-        self.meta = torch.zeros(W + 1, dtype=torch.int64, device=dev)
-        self.all_meta = torch.zeros(W * (W + 1), dtype=torch.int64, device=dev)
+        # {entries per owner..., records, entries dropped} per rank
+        self.meta = torch.zeros(W + 2, dtype=torch.int64, device=dev)
+        self.all_meta = torch.zeros(W * (W + 2), dtype=torch.int64, device=dev)
         self.seg_meta = torch.zeros((W, 2), dtype=torch.int64, device=dev)
         self.recv_ids = torch.zeros(W * seg_cap, dtype=torch.int32, device=dev)
         self.fs = torch.zeros(owner_cap + 2, dtype=torch.int64, device=dev)
@@ -357,7 +358,10 @@ class OwnerExchange:
         self.local.owner_bucket_device(W, C, self.map_cap, self.send, self.lid, self.meta,
                                        stream=stream)
         all_gather_flat(self.all_meta, self.meta, self.group)
-        am = self.all_meta.view(W, W + 1)
+        # any rank's dropped entries (segment or id-map overflow) shift the global ids
+        # of every rank: flag TCBEE_ESHARD here too, not only on the dropping rank
+        self.local.status_raise_device(self.all_meta[W + 1:], W, W + 2, stream=stream)
+        am = self.all_meta.view(W, W + 2)
         # segment r of what this rank receives: rank r's entries for it, rank r's records
         self.seg_meta[:, 0] = am[:, self.rank].clamp(max=C)
         self.seg_meta[:, 1] = am[:, W]

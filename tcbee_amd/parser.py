@@ -250,11 +250,21 @@ class PacketParser:
     def owner_bucket_device(self, world: int, seg_cap: int, map_cap: int, ent, lid, meta,
                             stream: int | None = None) -> None:
         """The table's flows into `world` owner segments of seg_cap entries (owner
-        exchange, contiguous shards); meta = {entries per owner..., records}."""
+        exchange, contiguous shards); meta (world + 2 words) = {entries per owner...,
+        records, entries dropped}."""
+        if meta.numel() < world + 2:
+            raise ValueError(f"owner meta needs world + 2 = {world + 2} words")
         _lib.check(_lib.lib().tcbee_owner_bucket_device(
             self._h, world, C.c_uint64(seg_cap), C.c_uint64(map_cap), _ptr(ent), _ptr(lid),
             _ptr(meta),
             C.c_void_p(stream or 0)), "tcbee_owner_bucket_device")
+
+    def status_raise_device(self, v, n: int, stride: int, stream: int | None = None) -> None:
+        """TCBEE_ESHARD on this context if any v[i * stride] (i < n, device u64) is
+        non-zero: a peer's dropped owner entries (OwnerExchange)."""
+        _lib.check(_lib.lib().tcbee_status_raise_device(
+            self._h, _ptr(v), C.c_uint64(n), C.c_uint64(stride), C.c_void_p(stream or 0)),
+            "tcbee_status_raise_device")
 
     def first_seen_device(self, out, cap: int, n_dev, stream: int | None = None) -> None:
         """out[id] = first_seen of flow id (ascending in id); n_dev = {flows, 0}."""

@@ -151,7 +151,7 @@ def run_flowhash(rank, world, port, n, cap, result_dir, filter_port):
 
 
 def run_gpu(rank, world, port, n, cap, result_dir, mode, n_flows=3000, filter_port=0,
-            backend="gloo"):
+            backend="gloo", map_caps=None):
     """N>1 choreography on the GPU: ranks share device 0 over gloo. mode "step":
     FlowMerge.step on one stream; mode "overlap": OverlappedMerge over 3 steps of
     the same shard (fresh table each step, output slots rotating), as bench.py;
@@ -160,7 +160,8 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode, n_flows=3000, filter_po
     mode "flowhash_real": the rank's flow-hash shard (host partitioner, the NIC-RSS
     step) of a mixed trace with rejected and FILTER_PORT-filtered frames, placed
     through the parse's record -> frame map; mode "flowhash_noframe": the same
-    without the map (must be refused: TCBEE_ESHARD)."""
+    without the map (must be refused: TCBEE_ESHARD). map_caps (mode "owner"): the
+    id-map size of each rank (default `cap` on every rank)."""
     import torch
     import torch.distributed as dist
 
@@ -218,7 +219,8 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode, n_flows=3000, filter_po
             from tcbee_amd.dist import OwnerExchange
             # per-owner segments: a rank holds at most `cap` flows, an owner about
             # 1/world of the global ones (generous here: tests cover small traces)
-            ox = OwnerExchange(p, mg, seg_cap=cap, owner_cap=cap, map_cap=cap,
+            ox = OwnerExchange(p, mg, seg_cap=cap, owner_cap=cap,
+                               map_cap=map_caps[rank] if map_caps else cap,
                                max_total_records=n)
             for i in range(2):  # the second step re-uses every buffer of the first
                 b = slots[0]

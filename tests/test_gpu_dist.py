@@ -291,6 +291,21 @@ def test_gpu_owner_exchange_map_overflow_is_refused(gpu, tmp_path):
         assert int(np.load(tmp_path / f"rank{r}.npz")["status"][0]) == _lib.ESHARD
 
 
+def test_gpu_owner_exchange_one_rank_overflows(gpu, tmp_path):
+    """Only rank 1's id map is too small: its dropped flows take no
+    segment slot (no phantom flow reaches an owner), and rank 0 — whose own table
+    fits — reports TCBEE_ESHARD too, since its global ids would be shifted."""
+    import torch.multiprocessing as mp
+
+    import dist_worker
+    from tcbee_amd import _lib
+    n, flows, cap, world = 90_000, 3000, 8192, 2
+    mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path), "owner",
+                                        flows, 0, "gloo", [cap, 1000]), nprocs=world, join=True)
+    for r in range(world):
+        assert int(np.load(tmp_path / f"rank{r}.npz")["status"][0]) == _lib.ESHARD, r
+
+
 @pytest.mark.parametrize("world,filter_port,direction", [(2, 0, 0), (3, 5201, 1)])
 def test_gpu_replay_pcap_sharded(gpu, oracle, tmp_path, world, filter_port, direction):
     """A pcap replayed over `world` ranks (contiguous shards, one pipeline each):

@@ -437,9 +437,11 @@ def test_config4_scale_over_1M_flows_mixed(gpu, oracle):
         assert p.status() == 0
 
 
-def test_config4_1M_flows_device_right_sized(gpu, oracle):
-    """1M synthetic IMIX flows, device-resident path, table sized exactly for 1M
-    flows (2^21 slots = 128 MiB: what bench.py allocates for config 4)."""
+@pytest.mark.parametrize("cap_mult", [1, 4])
+def test_config4_1M_flows_device_right_sized(gpu, oracle, cap_mult):
+    """1M synthetic IMIX flows, device-resident path; the table sized exactly for 1M
+    flows (max_flows = flows: 2^21 slots = 128 MiB, load 1/2) and at what bench.py
+    allocates for config 4 (max_flows = 4 x flows: 2^23 slots, load 1/8)."""
     import torch
     n, flows = 3_500_000, 1_000_000
     tr = tcbee_amd.synth_trace(n, sizes="imix", kind=1, n_flows=flows)
@@ -452,7 +454,7 @@ def test_config4_1M_flows_device_right_sized(gpu, oracle):
     fi_d = torch.empty(n, dtype=torch.int32, device="cuda")
     n_d = torch.zeros(1, dtype=torch.int64, device="cuda")
     ctr_d = torch.zeros(4, dtype=torch.int64, device="cuda")
-    with tcbee_amd.PacketParser(max_frames=n, max_flows=flows) as p:
+    with tcbee_amd.PacketParser(max_frames=n, max_flows=cap_mult * flows) as p:
         s = torch.cuda.current_stream().cuda_stream
         p.parse_device(d_arena, len(tr.arena), d_off, d_len, d_ts, n, rec_d, n, fh_d, fi_d, n_d,
                        ctr_d, stream=s)

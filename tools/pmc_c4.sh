@@ -18,8 +18,9 @@ run() {  # name counters... -- bench args
   echo "=== $name rc=$rc" >&2
   [ $rc -eq 0 ] || exit $rc
 }
-for leg in c3 c4 c4v8; do
+for leg in ${LEGS:-c3 c4 c4v8 v6}; do
   case $leg in
+    v6) args=(--sizes imix6) ;;
     c3) args=() ;;
     c4) args=(--config4) ;;
     c4v8) args=(--config4 --virtual-world 8) ;;

@@ -29,8 +29,26 @@ def pmc_values(path, kernel_sub):
     return [float(r["Counter_Value"]) for r in rows if kernel_sub in r["Kernel_Name"]]
 
 
+def leg_frames(leg: str) -> int:
+    """Frames per k_parse launch of a PMC leg: the bench's own "<n> frames resident"
+    log line (gpurun_out/pmc_<leg>_fetch.log, tools/pmc_c4.sh), else the nominal config size."""
+    import re
+    log = os.path.join(OUT, f"pmc_{leg}_fetch.log")
+    try:
+        m = re.search(r"rank 0: (\d+) frames resident", open(log).read())
+        if m:
+            return int(m.group(1))
+    except OSError:
+        pass
+    if leg == "c4v8":
+        sys.exit(f"{log}: no 'frames resident' line (the shard size is seed-dependent)")
+    return 100_000_000 if leg == "c3" else 125_000_000
+
+
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    if tag.startswith("-") or "/" in tag:
+        sys.exit(f"usage: {sys.argv[0]} ROUND_TAG  (a tag such as r03; got {tag!r})")
     os.makedirs(PROF, exist_ok=True)
     lines = [f"# rocprofv3 summary — {tag}", ""]
     stats = os.path.join(OUT, "prof", "run_kernel_stats.csv")
@@ -98,7 +116,9 @@ def main():
     legs = {"c3": ("config 3: 100M IMIX frames, 10k flows", ""),
             "c4": ("config 4, whole 1M-flow trace on one GPU: 125M IMIX frames", "--config4"),
             "c4v8": ("config 4, one GPU's flow-hash share at N=8: ~125M frames, ~125k flows",
-                     "--config4 --virtual-world 8")}
+                     "--config4 --virtual-world 8"),
+            "v6": ("config 3 over IPv6/TCP: 100M IMIX6 (78/576/1500) frames, 10k flows",
+                   "--sizes imix6")}
     pmc_legs = {}
     for leg, (what, args) in legs.items():
         paths = {k: os.path.join(OUT, f"pmc_{leg}_{k}", "run_counter_collection.csv")
@@ -112,7 +132,9 @@ def main():
             if "k_parse" in r["Kernel_Name"]:
                 rd.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
         rd = {k: statistics.median(v) for k, v in rd.items()}
-        frames = 100_000_000 if leg == "c3" else (125_000_000 if leg == "c4" else 124_967_316)
+        # frames the PMC'd k_parse launches parsed: from the leg's bench log ("N frames
+        # resident"), written beside the counter CSVs by tools/pmc_c4.sh
+        frames = leg_frames(leg)
         fetch, write = fk * 1024 * 2, wk * 1024
         pmc_legs[leg] = {"workload": what, "command": "bench.py --steps 2 --warmup 1 --no-cpu "
                          f"--no-extra --sample-check {args}".strip(), "frames": frames,
