@@ -155,12 +155,13 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     # flow-hash shards hold ~n_flows/world flows each; the exchange carries `xcap`
     # entries per rank (checked against the real count after the run)
     flows_here = -(-n_flows // sw) if flowhash else n_flows
-    # table: max_flows = 4x the shard's flows (>= 8 slots per flow, load <= 1/8).
-    # Linear-probe collisions cost K1 a random 64-B line each, and they grow with
-    # the load: at load 1/2 (max_flows = flows, 128 MiB for 1M flows) K1 is 6 %
-    # slower at 10k flows, 31 % at 125k and 36 % at 1M; 8x/16x gain < 3 % on K1 and
-    # lose it to the bigger per-step table reset (profiles/r02_capsweep.json)
-    cap = max(4 * flows_here, 64)
+    # table: max_flows = the shard's expected flows + 3 % + 64 (a flow-hash shard of
+    # config 3 at N=8 holds up to +3 % of the mean; claims past max_flows are
+    # refused). The compact table (round 3) keeps >= 2 slots per max_flow (load
+    # <= 1/2), 6 slots per 128-B line, so one probe is one line of a table of ~43 B
+    # per flow: 43 MB at 1M flows, resident in the Infinity Cache beside the stream
+    # (rounds 1-2: 64-B slots at max_flows = 4x flows, 512 MiB at 1M flows)
+    cap = max(flows_here + flows_here // 32 + 64, 64)
     # (the exchange carries up to xcap entries per rank: a quarter more than the
     # shard's expected flows)
     xcap = max(int(1.25 * flows_here) + 4096, 1 << 12)

@@ -30,7 +30,7 @@ struct tcbee_ctx {
   uint32_t pack_bits = 0;            // K1->K3 scratch packing (0: two words per record)
 
   FlowTable tab{};
-  uint64_t nslots = 0;
+  uint64_t nlines = 0;  // flow-table slot lines (6 slots of 16 B each)
   PersistState* d_persist = nullptr;
   BatchState* d_batch = nullptr;     // = d_batch_slot[slot] of the current batch
   // two slots of what a batch's K3 reads (batch state, K1 -> K3 scratch), so that
@@ -185,7 +185,8 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
   if (!c) return TCBEE_EINVAL;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  dfree(c->tab.meta);
+  dfree(c->tab.slots);
+  dfree(c->tab.ent);
   dfree(c->tab.cnt);
   dfree(c->tab.cmap);
   dfree(c->d_persist);
@@ -233,7 +234,9 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
 
 int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t max_arena,
                      uint64_t max_flows) {
-  if (!out || max_frames == 0 || max_frames > (1ull << 40)) return TCBEE_EINVAL;
+  if (!out || max_frames == 0) return TCBEE_EINVAL;
+  // batch-local record / frame indices are 31-bit (the flow table's fs32 words)
+  if (max_frames >= (1ull << 31)) return TCBEE_ECAPACITY;
   *out = nullptr;
   // 2^24 flows -> 2^25 slots = 2 GiB of table: K1's probe buffer resource and u32
   // slot offsets, and K3's bucketed mode (kMaxBuckets x kBucket claims), end there
@@ -265,16 +268,17 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   if (hipSetDevice(device) != hipSuccess) return fail(TCBEE_EDEVICE);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return fail(TCBEE_EDEVICE);
-  c->nslots = 64;
-  while (c->nslots < 2 * c->max_flows) c->nslots <<= 1;
-  c->tab.mask = c->nslots - 1;
+  // slots >= 2 x max_flows (load <= 1/2), 6 per 128-B line
+  c->nlines = (2 * c->max_flows + kSlotsPerLine - 1) / kSlotsPerLine;
+  c->tab.nlines = c->nlines;
+  c->tab.max_claims = c->max_flows;
   {
-    // claims < nslots: log2(nslots) bits + 1 (so no packed word is all ones, the
-    // no-flow mark); packed while at least 14 bits (caplen < 16383) remain
-    // (a standard Ethernet frame's 1518 B fits the 11 bits left at b = 21; longer
-    //  caplens saturate the field and go to the side array)
+    // claims < max_flows: ceil(log2(max_flows)) bits + 1 (so no packed word is all
+    // ones, the no-flow mark); packed while at least 11 bits remain (a standard
+    // Ethernet frame's 1518 B fits the 11 bits left at b = 21, max_flows <= 2^20;
+    // longer caplens saturate the field and go to the side array)
     uint32_t b = 1;
-    while ((1ull << (b - 1)) < c->nslots) ++b;
+    while ((1ull << (b - 1)) < c->max_flows) ++b;
     c->pack_bits = b <= 21 ? b : 0;
     if (const char* e = std::getenv("TCBEE_TEST_NOPACK")) c->pack_bits = std::atoi(e) ? 0 : c->pack_bits;
   }
@@ -282,9 +286,10 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   c->max_words = (max_frames + 31) / 32;
   c->max_sblocks = (c->max_words + kScanWordsPerBlock - 1) / kScanWordsPerBlock;
   hipError_t e = hipSuccess;
-  if ((e = dalloc(&c->tab.meta, 8 * c->nslots)) != hipSuccess) return fail(map_err(e));
-  if ((e = dalloc(&c->tab.cnt, 2 * c->nslots)) != hipSuccess) return fail(map_err(e));
-  if ((e = dalloc(&c->tab.cmap, c->nslots)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->tab.slots, 16 * c->nlines)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->tab.ent, 8 * c->max_flows)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->tab.cnt, 2 * c->max_flows)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->tab.cmap, c->max_flows)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_persist, 1)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_batch_slot[0], 1)) != hipSuccess) return fail(map_err(e));
   c->d_batch = c->d_batch_slot[0];
@@ -292,7 +297,7 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
     if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
       return fail(map_err(e));
   if ((e = dalloc(&c->d_tile_status, c->max_tiles)) != hipSuccess) return fail(map_err(e));
-  if ((e = dalloc(&c->d_new_list, c->nslots)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->d_new_list, c->max_flows)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_bitmap, c->max_words)) != hipSuccess) return fail(map_err(e));
   // all zero between batches from here on (K3 clears the words a batch set)
   if ((e = hipMemset(c->d_bitmap, 0, c->max_words * sizeof(uint32_t))) != hipSuccess)
@@ -314,7 +319,7 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   //  8 x (g1 / 8 / 2) groups x kRangeFlows claims; TCBEE_TEST_K3_NORANGE=1 keeps
   //  such tables on modes 1/2 — a test hook)
   uint64_t part_words = c->k3_g1max * kCountBins;
-  c->k3_range = c->nslots > (uint64_t)kCountBins;
+  c->k3_range = c->max_flows > (uint64_t)kCountBins;
   if (const char* e = std::getenv("TCBEE_TEST_K3_NORANGE")) c->k3_range = c->k3_range && !std::atoi(e);
   if (c->k3_range) {
     const uint64_t rows = (uint64_t)c->n_cu / 2;  // R >= 2 in mode 3: <= g1/16 groups x 8
@@ -323,10 +328,10 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   c->part_words = part_words;
   if ((e = dalloc(&c->d_count_part, part_words)) != hipSuccess)
     return fail(map_err(e));
-  if (c->nslots > (uint64_t)kCountBins && !c->k3_no_bucket) {
+  if (c->max_flows > (uint64_t)kCountBins && !c->k3_no_bucket) {
     // K3 mode 1 scratch: (claim, caplen) per frame, bucket offsets per K3 block,
     // partial rows of k_count_bucket (S x nb <= g2 rows of kBucket claims)
-    uint64_t nb = (c->nslots + kBucket - 1) / kBucket;
+    uint64_t nb = (c->max_flows + kBucket - 1) / kBucket;
     c->k3_nb_max = (uint32_t)(nb < kMaxBuckets ? nb : kMaxBuckets);
     c->k3_g2 = c->k3_nb_max > 2u * c->n_cu ? c->k3_nb_max : 2u * c->n_cu;
     if ((e = dalloc(&c->d_k3_region, max_frames)) != hipSuccess) return fail(map_err(e));
@@ -517,10 +522,11 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     k.lpart = c->d_k3_lpart;
     k.coffs = c->d_k3_coffs;
     k.chunk_off = c->k3_variant == 91 ? 1u : 0u;  // TCBEE_K3ABL=91: the two-pass scatter (A/B)
-    // 16384-record chunks (1024 threads, one workgroup per CU); TCBEE_K3ABL=92: 8192
-    // (512 threads, two per CU) — measured slower: 125k flows 5.60 vs 5.72 ms/step,
-    // 1M flows 7.51 vs 7.77 (shorter bucket runs for k_count_bucket, twice the chunks)
-    k.chunk = c->k3_variant == 92 ? 8192u : 16384u;
+    // 12288-record chunks in 76 KiB of LDS (k_count_chunk2: two workgroups per CU).
+    // A/B: TCBEE_K3ABL=93 the round-2 k_count_chunk (16384 records, 132 KiB, one
+    // workgroup per CU); 92: its 8192-record form (512 threads, two per CU) — slower
+    // in round 2 than 16384: 125k flows 5.60 vs 5.72 ms/step, 1M flows 7.51 vs 7.77
+    k.chunk = c->k3_variant == 92 ? 8192u : c->k3_variant == 93 ? 16384u : 12288u;
     // trade-off: more blocks = more latency hidden; each block writes a partial row
     // of every flow, so a block should see a few thousand records; and a block
     // never covers more than kK3MaxPer records (bin fields cannot overflow)
@@ -589,7 +595,7 @@ int tcbee_parse_finish_device(tcbee_ctx* c, const uint32_t* id_map_dev, uint64_t
   TRY_HIP(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   CountArgs k = c->pend;
-  if (id_map_dev && !c->d_omap) TRY_HIP(dalloc(&c->d_omap, c->nslots));
+  if (id_map_dev && !c->d_omap) TRY_HIP(dalloc(&c->d_omap, c->max_flows));
   hipStream_t ks = s;
   if (c->pend_ids) {  // async: after everything queued on `s` (K2, the id map)
     TRY_HIP(hipEventRecord(c->ev_fin, s));
@@ -597,7 +603,7 @@ int tcbee_parse_finish_device(tcbee_ctx* c, const uint32_t* id_map_dev, uint64_t
     ks = c->pend_ids;
   }
   if (id_map_dev) {
-    TRY_HIP(launch_compose(c->tab.cmap, id_map_dev, map_len, k.batch, c->d_omap, c->nslots, ks));
+    TRY_HIP(launch_compose(c->tab.cmap, id_map_dev, map_len, k.batch, c->d_omap, c->max_flows, ks));
     k.omap = c->d_omap;
   }
   c->count_pending = false;
@@ -782,33 +788,36 @@ int tcbee_flow_export(tcbee_ctx* c, tcbee_flow_entry* out, uint64_t cap, uint64_
   TRY_HIP(hipSetDevice(c->device));
   TRY_HIP(k3_wait_host(c));
   if (int rc = apply_pending_reset(c, c->stream)) return rc;
-  std::vector<uint64_t> meta, cnt;
+  PersistState p{};
+  TRY_HIP(hipMemcpyAsync(&p, c->d_persist, sizeof(p), hipMemcpyDeviceToHost, c->stream));
+  TRY_HIP(hipStreamSynchronize(c->stream));
+  const uint64_t nf = p.flow_count;
+  std::vector<uint64_t> ent, cnt;
+  std::vector<uint32_t> cmap;
   try {
-    meta.resize(8 * c->nslots);
-    cnt.resize(2 * c->nslots);
+    ent.resize(8 * nf + 1);
+    cnt.resize(2 * nf + 2);
+    cmap.resize(nf + 1);
   } catch (...) {
     return TCBEE_ENOMEM;
   }
-  PersistState p{};
-  TRY_HIP(hipMemcpyAsync(&p, c->d_persist, sizeof(p), hipMemcpyDeviceToHost, c->stream));
-  TRY_HIP(hipMemcpyAsync(meta.data(), c->tab.meta, meta.size() * 8, hipMemcpyDeviceToHost, c->stream));
-  TRY_HIP(hipMemcpyAsync(cnt.data(), c->tab.cnt, cnt.size() * 8, hipMemcpyDeviceToHost, c->stream));
-  TRY_HIP(hipStreamSynchronize(c->stream));
-  uint64_t written = 0;
-  for (uint64_t s = 0; s < c->nslots; ++s) {
-    const uint64_t* m = &meta[8 * s];
-    if (m[0] < 2 || m[7] == 0) continue;
-    const uint64_t id = m[7] - 1;
-    if (id >= cap) continue;
+  if (nf) {
+    TRY_HIP(hipMemcpyAsync(ent.data(), c->tab.ent, 8 * nf * 8, hipMemcpyDeviceToHost, c->stream));
+    TRY_HIP(hipMemcpyAsync(cnt.data(), c->tab.cnt, 2 * nf * 8, hipMemcpyDeviceToHost, c->stream));
+    TRY_HIP(hipMemcpyAsync(cmap.data(), c->tab.cmap, nf * 4, hipMemcpyDeviceToHost, c->stream));
+    TRY_HIP(hipStreamSynchronize(c->stream));
+  }
+  for (uint64_t cl = 0; cl < nf; ++cl) {  // claims; ids are a permutation of [0, nf)
+    const uint64_t* m = &ent[8 * cl];
+    const uint64_t id = cmap[cl];
+    if (id >= cap || id >= nf) continue;
     tcbee_flow_entry& e = out[id];
-    std::memcpy(e.tuple, m + 1, TCBEE_KEY_BYTES);
+    std::memcpy(e.tuple, m, TCBEE_KEY_BYTES);
     e.pkts = cnt[2 * id];
     e.bytes = cnt[2 * id + 1];
-    e.first_seen = m[6];
-    ++written;
+    e.first_seen = m[5];
   }
-  *n = p.flow_count < cap ? p.flow_count : cap;
-  (void)written;
+  *n = nf < cap ? nf : cap;
   return TCBEE_OK;
 }
 
@@ -855,8 +864,8 @@ int tcbee_flow_records_before_device(tcbee_ctx* c, const uint32_t* rec_frame_dev
   TRY_HIP(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if (int rc = apply_pending_reset(c, s)) return rc;
-  TRY_HIP(launch_records_before(c->tab, rec_frame_dev, frame_gidx_dev, n_rec_dev, n_rec_max,
-                                out_counts_dev, cap, s));
+  TRY_HIP(launch_records_before(c->tab, c->d_persist, rec_frame_dev, frame_gidx_dev, n_rec_dev,
+                                n_rec_max, out_counts_dev, cap, s));
   return TCBEE_OK;
 }
 
@@ -866,7 +875,7 @@ int tcbee_flow_set_first_seen_device(tcbee_ctx* c, const uint64_t* fs_by_id_dev,
   TRY_HIP(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if (int rc = apply_pending_reset(c, s)) return rc;
-  TRY_HIP(launch_set_first_seen(c->tab, fs_by_id_dev, cap, s));
+  TRY_HIP(launch_set_first_seen(c->tab, c->d_persist, fs_by_id_dev, cap, s));
   return TCBEE_OK;
 }
 
@@ -874,11 +883,13 @@ int tcbee_flow_merge_device(tcbee_ctx* c, const tcbee_flow_entry* ent_dev, uint6
                             uint64_t stride, const uint64_t* seg_meta_dev,
                             uint64_t max_total_records, uint32_t* out_ids_dev, void* stream) {
   if (!c || !seg_meta_dev || (nseg * stride && (!ent_dev || !out_ids_dev))) return TCBEE_EINVAL;
+  // merged first_seen values are min-reduced in the slots' 31-bit fs32 words
+  if (max_total_records >= (1ull << 31)) return TCBEE_ECAPACITY;
   const uint64_t total_records = max_total_records;
   TRY_HIP(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   const uint64_t words = (total_records + 31) / 32 + 1;
-  if (!c->d_mcnt) TRY_HIP(dalloc(&c->d_mcnt, 2 * c->nslots));
+  if (!c->d_mcnt) TRY_HIP(dalloc(&c->d_mcnt, 2 * c->max_flows));
   if (words > c->m_words) {
     // merge scratch grows with the global record count (not on the hot path)
     TRY_HIP(hipStreamSynchronize(s));
@@ -900,7 +911,7 @@ int tcbee_flow_merge_device(tcbee_ctx* c, const tcbee_flow_entry* ent_dev, uint6
   TRY_HIP(launch_table_init(c->tab, s));
   TRY_HIP(hipMemsetAsync(c->d_persist, 0, sizeof(PersistState), s));
   TRY_HIP(hipMemsetAsync(c->d_batch, 0, sizeof(BatchState), s));
-  TRY_HIP(hipMemsetAsync(c->d_mcnt, 0, 2 * c->nslots * sizeof(uint64_t), s));
+  TRY_HIP(hipMemsetAsync(c->d_mcnt, 0, 2 * c->max_flows * sizeof(uint64_t), s));
   MergeArgs g{};
   g.ent = reinterpret_cast<const uint64_t*>(ent_dev);
   g.nseg = nseg;

@@ -13,22 +13,40 @@ namespace tcbee {
 //   rejected frames without a record -> frame map)
 constexpr uint32_t kStFlowFull = 1u, kStSpin = 2u, kStShard = 4u;
 
-// Flow table in HBM, open addressing, linear probing, power-of-two slots.
-//  meta[s*8 + 0] tag word: 0 empty, 1 busy, else hash_tag32(h) | claim << 32,
-//                      claim = the flow's dense claim index (insertion order over
-//                      the context's life, fixed at insert; cmap[claim] = dense id)
-//  meta[s*8 + 1..5]    the 40-B key as 5 LE u64 words
-//  meta[s*8 + 6]       first_seen (global accepted-frame index, ~0 = none)
-//  meta[s*8 + 7]       dense flow id + 1 (0 = not yet assigned)
-//  cnt [id*2 + 0/1]    pkts / bytes of dense flow id `id` (by id, not slot:
-//                      k_count histograms them per dense id)
+// Flow table in HBM (round 3): compact slot lines probed by K1, plus dense
+// per-claim entries. A flow's claim index is its insertion order over the
+// context's life (fixed at insert; cmap[claim] = its dense first-seen id), so
+// claims are dense in [0, flows) and bounded by max_claims (= max_flows).
+//  slots: nlines lines of 128 B (u64[16]); open addressing, linear probing over
+//    slot s = line * 6 + pos:
+//    words 2*pos, 2*pos + 1 (pos < 6): w0, w1 of slot pos
+//      w1 = kind << 56 | claim << 32 | lo32 (w1 == 0: empty; kind 1: busy)
+//      kind 2: an IPv4-form key (12 zero bytes + the address, xdp.rs:116-119):
+//              w0 = saddr | daddr << 32 (wire bytes), lo32 = sport | dport << 16 —
+//              the slot holds the whole key, so the slot alone decides a match
+//      kind 3: any other key: w0 = flow_hash64, lo32 = 0; the key is ent[claim]
+//      kind 4/5: dead (2/3 refused because the table was full): the key's w0 and
+//              lo32, no claim — the flow's later frames find it and stay unclassified
+//    bytes 96 + 4*pos: fs32 of slot pos: the batch-local first record index of a
+//      flow new in this batch (kFs32Flag | frame while only its claimer's mark is
+//      known); stale for flows of earlier batches (never read for them)
+//    One probe = one line (16-B slot + its fs32): ~43 B of table per flow at load
+//    1/2 instead of the 64-B slots of rounds 1-2 (512 MiB at 1M flows, which no
+//    cache kept; 43 MB stays in the 256 MiB Infinity Cache beside the stream).
+//  ent [claim*8 + 0..4] the 40-B key as 5 LE u64 words; [claim*8 + 5] first_seen
+//      (global accepted-record index, written by K2); 6..7 spare
+//  cnt [id*2 + 0/1]    pkts / bytes of dense flow id `id`
 struct FlowTable {
-  uint64_t* meta;
+  uint64_t* slots;
+  uint64_t nlines;
+  uint64_t* ent;
   uint64_t* cnt;
-  uint64_t mask;  // slots - 1
-  uint32_t* cmap;  // claim index -> dense id (0-based), written by K2; dense in
-                   // [0, flows), so K3 stages it in LDS
+  uint32_t* cmap;        // claim index -> dense id (0-based), written by K2; dense in
+                         // [0, flows), so K3 stages it in LDS
+  uint64_t max_claims;   // claims at or past it are refused (TCBEE_EFLOWFULL)
 };
+constexpr uint32_t kSlotsPerLine = 6;
+constexpr uint32_t kFs32Flag = 1u << 31;
 
 // Lives across batches of one context.
 struct PersistState {
@@ -159,8 +177,8 @@ struct MergeArgs {
   BatchState* batch;
   PersistState* persist;
   uint64_t* new_list;
-  uint64_t* mcnt;             // per-slot pkts/bytes (2 * slots), zeroed
-  uint32_t* out_slot;         // per entry: slot, then merged id
+  uint64_t* mcnt;             // per-claim pkts/bytes (2 * max_claims), zeroed
+  uint32_t* out_slot;         // per entry: claim, then merged id
   uint32_t* bitmap;           // merge first-seen bitmap (cleared after use)
 };
 hipError_t launch_export(FlowTable t, uint64_t* out, uint64_t cap, const PersistState* p,
@@ -183,12 +201,12 @@ struct GlobalExportArgs {
 hipError_t launch_export_global(const GlobalExportArgs& g, hipStream_t s);
 // Merged table (first_seen = global frame index): out[id] = number of this
 // rank's records whose global frame index is below the flow's first_seen.
-hipError_t launch_records_before(FlowTable t, const uint32_t* rec_frame,
+hipError_t launch_records_before(FlowTable t, const PersistState* p, const uint32_t* rec_frame,
                                  const uint64_t* frame_gidx, const uint64_t* n_rec,
                                  uint64_t n_rec_max, uint64_t* out, uint64_t cap, hipStream_t s);
 // first_seen of flow id := fs_by_id[id] (ids < cap)
-hipError_t launch_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t cap,
-                                 hipStream_t s);
+hipError_t launch_set_first_seen(FlowTable t, const PersistState* p, const uint64_t* fs_by_id,
+                                 uint64_t cap, hipStream_t s);
 // Flow-hash exchange: first frame per local id (GlobalExportArgs.out = u64[cap]);
 // global ids from the all-gathered first-frame arrays; output-id composition.
 hipError_t launch_first_frames(const GlobalExportArgs& g, hipStream_t s);

@@ -305,75 +305,131 @@ __device__ __forceinline__ bool parse_window(const uint8_t* __restrict__ arena, 
 }
 
 // ---------------------------------------------------------------------------
-// Flow-table upsert. Identity = full 40-B key; the 64-bit tag only filters.
-// Claim protocol: CAS tag empty->busy, key words by agent-scope stores, drain,
-// then the tag (agent-scope store). Readers poll the tag relaxed (agent) and
-// read the key by agent-scope loads; a mismatch is re-checked at the coherence
-// point before the probe moves on (never a duplicate flow).
+// Flow table (tcbee_internal.h): compact slot lines + per-claim entries.
 // ---------------------------------------------------------------------------
-// first_seen word while a flow's first record index is not known yet: the
-// claimer stores kFsFlag | its frame index with the key, so later readers of a
-// hot new flow can tell locally whether they precede the claimer (and only
-// those contend on the atomicMin) instead of all seeing "unset".
-constexpr uint64_t kFsFlag = 1ull << 63;
-
-__device__ __forceinline__ bool fs_needs_min(uint64_t fs_seen, uint64_t frame_i, uint64_t gidx) {
-  if (fs_seen & kFsFlag) return (fs_seen & ~kFsFlag) >= frame_i;  // the claimer or earlier
-  return gidx < fs_seen;
+__device__ __forceinline__ uint32_t ld_agent32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent32(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr uint64_t kKindBusy = 1ull << 56;
+constexpr uint64_t kClaimBits = 0xFFFFFFull << 32;  // w1 bits 55:32
+__device__ __forceinline__ uint32_t slot_line(uint32_t s) { return __umulhi(s, 0xAAAAAAABu) >> 2; }  // s / 6
+__device__ __forceinline__ uint64_t* slot_ptr(const FlowTable& T, uint32_t s) {
+  const uint32_t l = slot_line(s);
+  return T.slots + 16ull * l + 2u * (s - l * kSlotsPerLine);
+}
+__device__ __forceinline__ uint32_t* slot_fs(const FlowTable& T, uint32_t s) {
+  const uint32_t l = slot_line(s);
+  return reinterpret_cast<uint32_t*>(T.slots + 16ull * l + 12) + (s - l * kSlotsPerLine);
+}
+// home slot: line from the hash's high word (range reduction), position from its low bits
+__device__ __forceinline__ uint32_t home_slot(uint64_t h, uint64_t nlines) {
+  const uint32_t line = (uint32_t)(((h >> 32) * nlines) >> 32);
+  return line * kSlotsPerLine + (uint32_t)(((h & 0xFFFFFFull) * kSlotsPerLine) >> 24);
+}
+// the slot words that name key K: w0 and the kind | lo32 bits of w1 (all but the claim)
+__device__ __forceinline__ void key_slot_words(const uint64_t (&K)[5], uint64_t h, uint64_t& w0,
+                                               uint64_t& kl) {
+  if ((K[0] | K[2] | (K[1] & 0xFFFFFFFFull) | (K[3] & 0xFFFFFFFFull)) == 0) {  // IPv4 form
+    w0 = (K[1] >> 32) | (K[3] & 0xFFFFFFFF00000000ull);
+    kl = (2ull << 56) | (uint32_t)K[4];  // sport | dport << 16 (protocol is always 6)
+  } else {
+    w0 = h;
+    kl = 3ull << 56;
+  }
 }
 
-// Returns the slot (~0 on failure); `claim` = the flow's claim index (tag word
-// bits 63:32): flow_count before this batch + its position in this batch's
-// new-flow list, fixed before the tag is published.
+// first_seen (fs32) while a flow's first record index is not known yet: the
+// claimer stores kFs32Flag | its frame index, so later readers of a hot new flow
+// can tell locally whether they precede the claimer (and only those contend on the
+// atomicMin) instead of all seeing "unset". Batch-local: batches stay < 2^31 frames.
+__device__ __forceinline__ bool fs_needs_min(uint32_t fs_seen, uint32_t frame_i, uint32_t p) {
+  if (fs_seen & kFs32Flag) return (fs_seen & ~kFs32Flag) >= frame_i;  // the claimer or earlier
+  return p < fs_seen;
+}
+
+// Flow-table upsert; identity = the full 40-B key. Returns the slot (~0 on
+// failure); `claim` = the flow's claim index (flow_count before this batch + its
+// position in this batch's new-flow list), fixed before the slot is published.
+// Claim protocol: CAS w1 empty -> busy, the entry (key) and the slot's fs32 mark
+// and w0 by agent-scope stores, drain, then w1 (agent-scope store). Readers poll
+// w1 relaxed; a key that lives in the entry (kind 3) is compared by agent-scope
+// loads and a mismatch re-checked at the coherence point before the probe moves
+// on (never a duplicate flow). The slot's line holds w0, w1 and fs32 together, so
+// a snapshot that shows a published w1 shows its w0 and mark.
 __device__ uint32_t flow_upsert(const FlowTable& T, const uint64_t (&K)[5], uint64_t h,
                                 BatchState* batch, uint64_t* new_list, PersistState* persist,
-                                uint64_t& fs_seen, uint32_t& claim, uint64_t claim_mark = ~0ull) {
-  const uint32_t tag = hash_tag32(h);
-  uint64_t s = h & T.mask;
-  for (uint64_t probe = 0; probe <= T.mask; ++probe) {
-    uint64_t* m = T.meta + s * 8;
-    uint64_t cur = ld_agent(m);
-    if (cur == kTagEmpty) {
-      uint64_t expected = kTagEmpty;
-      if (__hip_atomic_compare_exchange_strong(m, &expected, kTagBusy, __ATOMIC_RELAXED,
+                                uint64_t fbase, uint32_t& fs_seen, uint32_t& claim,
+                                uint32_t claim_mark = 0xFFFFFFFFu) {
+  uint64_t w0k, kl;
+  key_slot_words(K, h, w0k, kl);
+  const bool in_ent = (kl >> 56) == 3;
+  const uint32_t nslots = (uint32_t)T.nlines * kSlotsPerLine;
+  uint32_t s = home_slot(h, T.nlines);
+  for (uint32_t probe = 0; probe < nslots; ++probe) {
+    uint64_t* m = slot_ptr(T, s);
+    uint64_t cur = ld_agent(m + 1);
+    if (cur == 0) {
+      uint64_t expected = 0;
+      if (__hip_atomic_compare_exchange_strong(m + 1, &expected, kKindBusy, __ATOMIC_RELAXED,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         const uint64_t slot_no = atomicAdd((unsigned long long*)&batch->n_new, 1ull);
+        const uint64_t cl = fbase + slot_no;
+        if (cl >= T.max_claims) {
+          // table full: published dead (this key, no claim), so the flow's later
+          // frames find it instead of claiming again
+          st_agent(m, w0k);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          st_agent(m + 1, kl + (2ull << 56));
+          atomicOr(&persist->status, kStFlowFull);
+          return 0xFFFFFFFFu;
+        }
         new_list[slot_no] = s;
-        claim = (uint32_t)(persist->flow_count + slot_no);
+        claim = (uint32_t)cl;
+        uint64_t* e = T.ent + 8 * cl;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) st_agent(m + 1 + j, K[j]);
-        st_agent(m + 6, claim_mark);
+        for (int j = 0; j < 5; ++j) st_agent(e + j, K[j]);
+        st_agent32(slot_fs(T, s), claim_mark);
+        st_agent(m, w0k);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        st_agent(m, (uint64_t)tag | ((uint64_t)claim << 32));
+        st_agent(m + 1, kl | (cl << 32));
         fs_seen = claim_mark;
-        return (uint32_t)s;
+        return s;
       }
       cur = expected;
     }
-    for (uint32_t spins = 0; cur == kTagBusy; ++spins) {
+    for (uint32_t spins = 0; cur == kKindBusy; ++spins) {
       if (spins > kSpinLimit) {
         atomicOr(&persist->status, kStSpin);
         return 0xFFFFFFFFu;
       }
       __builtin_amdgcn_s_sleep(1);
-      cur = ld_agent(m);
+      cur = ld_agent(m + 1);
     }
-    if ((uint32_t)cur == tag) {
+    const uint64_t ckl = cur & ~kClaimBits;
+    if ((ckl == kl || ckl == kl + (2ull << 56)) && ld_agent(m) == w0k) {
+      if (ckl != kl) return 0xFFFFFFFFu;  // dead slot of this key: the table was full
+      const uint32_t c = (uint32_t)((cur & kClaimBits) >> 32);
       bool eq = true;
+      if (in_ent) {
+        uint64_t* e = T.ent + 8ull * c;
 #pragma unroll
-      for (int j = 0; j < 5; ++j) eq = eq && (ld_agent(m + 1 + j) == K[j]);
-      if (!eq) {
-        eq = true;
+        for (int j = 0; j < 5; ++j) eq = eq && (ld_agent(e + j) == K[j]);
+        if (!eq) {
+          eq = true;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) eq = eq && (ld_coherent(m + 1 + j) == K[j]);
+          for (int j = 0; j < 5; ++j) eq = eq && (ld_coherent(e + j) == K[j]);
+        }
       }
       if (eq) {
-        fs_seen = ld_agent(m + 6);
-        claim = (uint32_t)(cur >> 32);
-        return (uint32_t)s;
+        fs_seen = ld_agent32(slot_fs(T, s));
+        claim = c;
+        return s;
       }
     }
-    s = (s + 1) & T.mask;
+    s = s + 1 == nslots ? 0u : s + 1;
   }
   atomicOr(&persist->status, kStFlowFull);
   return 0xFFFFFFFFu;
@@ -558,12 +614,14 @@ void k_parse(ParseArgs a) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint64_t tile = blockIdx.x;
   const uint64_t i0 = tile * (uint64_t)TILE;
-  const uint64_t rec_base = a.persist->rec_base;
+  // flows claimed before this batch (claims below it have first records in earlier
+  // batches: their frames never compete for first_seen)
+  const uint64_t fbase = FLOWS ? a.persist->flow_count : 0;
 
   uint32_t R[FPL][19];
   bool acc[FPL];
   uint32_t rank[FPL], slot[FPL], hsh[FPL], clen[FPL], claim[FPL];
-  uint64_t fs_seen[FPL];
+  uint32_t fs_seen[FPL];
   uint64_t K[FPL][5];
 
   // phase A: index loads of all the lane's frames, then all their header-window
@@ -576,7 +634,7 @@ void k_parse(ParseArgs a) {
     slot[f] = 0xFFFFFFFFu;
     claim[f] = 0xFFFFFFFFu;
     hsh[f] = 0;
-    fs_seen[f] = ~0ull;
+    fs_seen[f] = 0xFFFFFFFFu;
 #pragma unroll
     for (int j = 0; j < 5; ++j) K[f][j] = 0;
     const bool in = i < a.n;
@@ -624,12 +682,12 @@ void k_parse(ParseArgs a) {
   if (!(ABL & 1) && !withhold && tid == 0) lookback_publish(a.tile_status, tile, total);
 
   if (FLOWS) {
-    // phase B: hash, then issue the first probe's slot-line loads of every frame
-    uint64_t h[FPL], W[FPL][7];
-    // num_records = table bytes (<= 2 GiB: tcbee_ctx_create caps max_flows at
-    // kMaxTableFlows, so slot offsets fit u32); the bits are read as unsigned
-    const __amdgpu_buffer_rsrc_t meta_rs = __builtin_amdgcn_make_buffer_rsrc(
-        a.tab.meta, 0, (int)(uint32_t)((a.tab.mask + 1) * 64u), 0x00020000);
+    // phase B: hash, then issue the first probe's slot loads of every frame
+    uint64_t h[FPL], W0[FPL], W1[FPL];
+    uint32_t FS[FPL], S0[FPL];
+    // num_records = the slot lines' bytes (< 2^30: max_flows <= kMaxTableFlows)
+    const __amdgpu_buffer_rsrc_t sl_rs = __builtin_amdgcn_make_buffer_rsrc(
+        a.tab.slots, 0, (int)(uint32_t)(a.tab.nlines * 128u), 0x00020000);
     bool uni[FPL], want[FPL];
     uint32_t leader[FPL];
 #pragma unroll
@@ -645,73 +703,76 @@ void k_parse(ParseArgs a) {
       if (acc[f]) hsh[f] = fold32(h[f]);
       want[f] = uni[f] ? lane == leader[f] : acc[f];
       if (want[f]) {
-        // The 64-B slot as 4 x 16-B loads. Plain (cacheable) loads are exact here:
-        // a slot never straddles a cache line and the claimer stores the key
-        // (drained) before the tag, so any snapshot that shows this flow's tag
-        // also shows its key; a stale snapshot shows EMPTY/BUSY or a mismatch,
-        // and every such miss falls through to flow_upsert's coherent path.
-        const uint32_t off = (uint32_t)((h[f] & a.tab.mask) * 64u);
-        u32x4 q[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = __builtin_amdgcn_raw_buffer_load_b128(meta_rs, off + 16u * j, 0, PROBE_AUX);
-#pragma unroll
-        for (int j = 0; j < 7; ++j) {
-          const u32x4 v = q[j >> 1];
-          W[f][j] = (j & 1) ? ((uint64_t)v[2] | ((uint64_t)v[3] << 32)) : ((uint64_t)v[0] | ((uint64_t)v[1] << 32));
-        }
+        // The 16-B slot and its fs32 (one line). Plain (cacheable) loads are exact
+        // here: the claimer stores w0 and the fs32 mark (drained) before w1, all in
+        // one line, so any snapshot that shows this flow's w1 shows its w0 and mark;
+        // a stale snapshot shows EMPTY/BUSY or a mismatch, and every such miss falls
+        // through to flow_upsert's coherent path.
+        S0[f] = home_slot(h[f], a.tab.nlines);
+        const uint32_t l = slot_line(S0[f]), pos = S0[f] - l * kSlotsPerLine;
+        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(sl_rs, l * 128u + 16u * pos, 0, PROBE_AUX);
+        FS[f] = __builtin_amdgcn_raw_buffer_load_b32(sl_rs, l * 128u + 96u + 4u * pos, 0, PROBE_AUX);
+        W0[f] = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
+        W1[f] = (uint64_t)q[2] | ((uint64_t)q[3] << 32);
       }
     }
-    // phase C: resolve; a miss (new flow, collision, busy slot) takes the full upsert
+    // phase C: resolve; a miss (new flow, busy slot, an entry-held key) takes the
+    // full upsert
+    const uint32_t nslots = (uint32_t)a.tab.nlines * kSlotsPerLine;
+    // entries: 64 B per claim (< 1 GiB: max_claims <= kMaxTableFlows)
+    const __amdgpu_buffer_rsrc_t ent_rs = __builtin_amdgcn_make_buffer_rsrc(
+        a.tab.ent, 0, (int)(uint32_t)(a.tab.max_claims * 64u), 0x00020000);
 #pragma unroll
     for (int f = 0; f < FPL; ++f) {
-      uint32_t sl = 0xFFFFFFFFu, cl = 0xFFFFFFFFu;
-      uint64_t fs = ~0ull;
+      uint32_t sl = 0xFFFFFFFFu, cl = 0xFFFFFFFFu, fs = 0xFFFFFFFFu;
       if (want[f]) {
-        const bool hit = (uint32_t)W[f][0] == hash_tag32(h[f]) && W[f][1] == K[f][0] &&
-                         W[f][2] == K[f][1] && W[f][3] == K[f][2] && W[f][4] == K[f][3] &&
-                         W[f][5] == K[f][4];
-        if (hit) {
-          sl = (uint32_t)(h[f] & a.tab.mask);
-          fs = W[f][6];
-          cl = (uint32_t)(W[f][0] >> 32);
-        } else {
-          // Walk on with plain loads while the slots hold OTHER flows (a published
-          // tag word of another hash; a tag equal to ours with another key goes to
-          // the coherent path). Within a batch a slot only
-          // goes EMPTY -> BUSY -> published, so a published foreign slot seen in
-          // any snapshot is foreign for good; EMPTY/BUSY may be stale and end the
-          // walk. Collisions of existing flows thus stay off the atomic path.
-          const uint32_t mytag = hash_tag32(h[f]);
-          uint64_t s = h[f] & a.tab.mask;
-          uint64_t cur0 = W[f][0];
-          bool slow = true;
-          for (uint32_t step = 0; step < a.plain_walk; ++step) {
-            if (cur0 < 2 || (uint32_t)cur0 == mytag) break;
-            s = (s + 1) & a.tab.mask;
-            u32x4 q[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              q[j] = __builtin_amdgcn_raw_buffer_load_b128(meta_rs, (uint32_t)(s * 64u) + 16u * j, 0, PROBE_AUX);
-            uint64_t V[7];
-#pragma unroll
-            for (int j = 0; j < 7; ++j) {
-              const u32x4 v = q[j >> 1];
-              V[j] = (j & 1) ? ((uint64_t)v[2] | ((uint64_t)v[3] << 32)) : ((uint64_t)v[0] | ((uint64_t)v[1] << 32));
+        uint64_t w0k, kl;
+        key_slot_words(K[f], h[f], w0k, kl);
+        // Walk with plain loads while the slots hold OTHER flows (published, another
+        // key); within a batch a slot only goes EMPTY -> BUSY -> published, so a
+        // published foreign slot seen in any snapshot is foreign for good;
+        // EMPTY/BUSY may be stale and end the walk. A kind-2 (IPv4-form) slot
+        // decides alone; a kind-3 candidate (same 64-bit hash) needs its entry
+        // compared, and goes to the coherent path.
+        uint32_t s = S0[f];
+        uint64_t w0 = W0[f], w1 = W1[f];
+        uint32_t fsv = FS[f];
+        bool slow = true;
+        for (uint32_t step = 0;; ++step) {
+          if (w1 <= kKindBusy) break;
+          if ((w1 & ~kClaimBits) == kl && w0 == w0k) {
+            const uint32_t c = (uint32_t)((w1 & kClaimBits) >> 32);
+            bool eq = true;
+            if ((kl >> 56) == 3) {  // same 64-bit hash: the entry decides (plain loads;
+                                    // a stale line mismatches and takes the slow path)
+              const u32x4 e0 = __builtin_amdgcn_raw_buffer_load_b128(ent_rs, c * 64u, 0, PROBE_AUX);
+              const u32x4 e1 = __builtin_amdgcn_raw_buffer_load_b128(ent_rs, c * 64u + 16u, 0, PROBE_AUX);
+              const u32x4 e2 = __builtin_amdgcn_raw_buffer_load_b128(ent_rs, c * 64u + 32u, 0, PROBE_AUX);
+              eq = K[f][0] == ((uint64_t)e0[0] | ((uint64_t)e0[1] << 32)) &&
+                   K[f][1] == ((uint64_t)e0[2] | ((uint64_t)e0[3] << 32)) &&
+                   K[f][2] == ((uint64_t)e1[0] | ((uint64_t)e1[1] << 32)) &&
+                   K[f][3] == ((uint64_t)e1[2] | ((uint64_t)e1[3] << 32)) &&
+                   K[f][4] == ((uint64_t)e2[0] | ((uint64_t)e2[1] << 32));
             }
-            cur0 = V[0];
-            if ((uint32_t)V[0] == mytag && V[1] == K[f][0] && V[2] == K[f][1] && V[3] == K[f][2] &&
-                V[4] == K[f][3] && V[5] == K[f][4]) {
-              sl = (uint32_t)s;
-              fs = V[6];
-              cl = (uint32_t)(V[0] >> 32);
+            if (eq) {
+              sl = s;
+              cl = c;
+              fs = fsv;
               slow = false;
-              break;
             }
+            break;
           }
-          if (slow)
-            sl = flow_upsert(a.tab, K[f], h[f], a.batch, a.new_list, a.persist, fs, cl,
-                             kFsFlag | (i0 + (uint64_t)f * BLK + tid));
+          if (step >= a.plain_walk) break;
+          s = s + 1 == nslots ? 0u : s + 1;
+          const uint32_t l = slot_line(s), pos = s - l * kSlotsPerLine;
+          const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(sl_rs, l * 128u + 16u * pos, 0, PROBE_AUX);
+          fsv = __builtin_amdgcn_raw_buffer_load_b32(sl_rs, l * 128u + 96u + 4u * pos, 0, PROBE_AUX);
+          w0 = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
+          w1 = (uint64_t)q[2] | ((uint64_t)q[3] << 32);
         }
+        if (slow)
+          sl = flow_upsert(a.tab, K[f], h[f], a.batch, a.new_list, a.persist, fbase, fs, cl,
+                           kFs32Flag | (uint32_t)(i0 + (uint64_t)f * BLK + tid));
       }
       if (uni[f]) {
         slot[f] = __shfl(sl, leader[f]);
@@ -798,19 +859,20 @@ void k_parse(ParseArgs a) {
       }
     }
     if (FLOWS) {
-      const bool mine = acc[f] && slot[f] != 0xFFFFFFFFu;
+      // first_seen competition: only flows new in this batch (claim >= fbase)
+      const bool mine = acc[f] && slot[f] != 0xFFFFFFFFu && claim[f] >= fbase;
       const uint64_t am = __ballot(mine);
       if (am) {
         const uint32_t leader = (uint32_t)__ffsll((unsigned long long)am) - 1;
         const uint32_t s0 = __shfl(slot[f], leader);
-        const uint64_t gidx = rec_base + p;
-        const uint64_t frame_i = i0 + (uint64_t)f * BLK + tid;
+        const uint32_t p32 = (uint32_t)p;
+        const uint32_t frame_i = (uint32_t)(i0 + (uint64_t)f * BLK + tid);
         if (__all(!mine || slot[f] == s0)) {
           // leader = lowest rank of the wave = its smallest accepted index
-          if (lane == leader && fs_needs_min(fs_seen[f], frame_i, gidx))
-            atomicMin((unsigned long long*)&a.tab.meta[8ull * s0 + 6], (unsigned long long)gidx);
-        } else if (mine && fs_needs_min(fs_seen[f], frame_i, gidx)) {
-          atomicMin((unsigned long long*)&a.tab.meta[8ull * slot[f] + 6], (unsigned long long)gidx);
+          if (lane == leader && fs_needs_min(fs_seen[f], frame_i, p32))
+            atomicMin(slot_fs(a.tab, s0), p32);
+        } else if (mine && fs_needs_min(fs_seen[f], frame_i, p32)) {
+          atomicMin(slot_fs(a.tab, slot[f]), p32);
         }
       }
     }
@@ -821,16 +883,11 @@ void k_parse(ParseArgs a) {
 // flow table init: tags/keys/ids 0, first_seen ~0, counters 0
 // ---------------------------------------------------------------------------
 __global__ void k_table_init(FlowTable t) {
-  const uint64_t nslots = t.mask + 1;
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < nslots;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t* m = t.meta + 8 * s;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) m[j] = 0;
-    m[6] = ~0ull;
-    t.cnt[2 * s] = 0;  // ids < slots: the by-id counters share the index range
-    t.cnt[2 * s + 1] = 0;
-  }
+  const uint64_t words = 16 * t.nlines;  // slot lines: every w1 (and fs32) zero = empty
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  for (uint64_t w = t0; w < words; w += stride) t.slots[w] = 0;
+  for (uint64_t i = t0; i < 2 * t.max_claims; i += stride) t.cnt[i] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -845,15 +902,12 @@ __global__ void k_prep(PrepArgs p) {
   //  K3 clears the words the rank step set)
   if (p.reset) {
     if (t0 < sizeof(PersistState) / 8) reinterpret_cast<uint64_t*>(p.persist)[t0] = 0;
-    const uint64_t nslots = p.tab.mask + 1;
-    for (uint64_t s = t0; s < nslots; s += stride) {
-      uint64_t* m = p.tab.meta + 8 * s;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) m[j] = 0;
-      m[6] = ~0ull;
-      // (the by-id counters are zeroed by K2 as ids are handed out: the previous
-      //  batch's K3 may still be adding to them on another stream)
-    }
+    // empty slot lines (16 B of slot lines per 16-B store); entries need nothing
+    // (claims restart at 0), and the by-id counters are zeroed by K2 as ids are
+    // handed out (the previous batch's K3 may still be adding to them on another
+    // stream)
+    uint4* L = reinterpret_cast<uint4*>(p.tab.slots);
+    for (uint64_t q = t0; q < 8 * p.tab.nlines; q += stride) L[q] = make_uint4(0u, 0u, 0u, 0u);
   }
 }
 
@@ -867,15 +921,29 @@ __global__ void k_prep(PrepArgs p) {
 //    a contiguous word range read 64 consecutive words at a time (coalesced).
 constexpr uint32_t kRankSortMax = 2048;
 
+// new flows this batch that got a claim (claims past max_claims were refused:
+// their slots are dead, nothing was written to new_list for them)
+__device__ __forceinline__ uint64_t rank_new(const RankArgs& r, uint64_t fbase) {
+  const uint64_t n = r.batch->n_new;
+  const uint64_t room = r.tab.max_claims > fbase ? r.tab.max_claims - fbase : 0;
+  return n < room ? n : room;
+}
+// the batch-local first record index of new flow j (its slot's fs32)
+__device__ __forceinline__ uint32_t new_flow_fs(const RankArgs& r, uint64_t j) {
+  return *slot_fs(r.tab, (uint32_t)r.new_list[j]);
+}
+
 // End of a single-block rank: the batch is classified — advance the context's
 // record base and flow count (K1 of the next batch reads them; K3 no longer does)
 __device__ __forceinline__ void rank_done(const RankArgs& r, uint32_t tid, uint64_t base,
                                           uint64_t fbase, uint64_t n_new) {
-  if (!r.update_persist) return;
-  __syncthreads();  // every thread has read the old base / fbase
+  __syncthreads();  // every thread has read the old base / fbase / n_new
   if (tid == 0) {
-    r.persist->rec_base = base + r.batch->n_acc;
-    r.persist->flow_count = fbase + n_new;
+    r.batch->n_new = n_new;  // the claimed ones (readers after K2 see the clamp)
+    if (r.update_persist) {
+      r.persist->rec_base = base + r.batch->n_acc;
+      r.persist->flow_count = fbase + n_new;
+    }
   }
 }
 
@@ -883,13 +951,12 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
   __shared__ uint32_t s_fs[kRankSortMax];
   __shared__ uint32_t s_tmp[16];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint64_t n_new = r.batch->n_new;
   const uint64_t base = r.persist->rec_base;
   const uint64_t fbase = r.persist->flow_count;
+  const uint64_t n_new = rank_new(r, fbase);
   if (tid == 0) r.batch->flow_total = fbase + n_new;
   if (n_new <= kRankSortMax) {
-    for (uint32_t j = tid; j < n_new; j += 1024)
-      s_fs[j] = (uint32_t)(r.tab.meta[8 * r.new_list[j] + 6] - base);
+    for (uint32_t j = tid; j < n_new; j += 1024) s_fs[j] = new_flow_fs(r, j);
     for (uint32_t j = (uint32_t)n_new + tid; j < ((uint32_t)n_new + 3u) / 4u * 4u; j += 1024)
       s_fs[j] = 0xFFFFFFFFu;  // pad to a multiple of 4 (never below a real value)
     __syncthreads();
@@ -902,8 +969,7 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
         const uint4 q = v4[i];
         rank += (q.x < v) + (q.y < v) + (q.z < v) + (q.w < v);
       }
-      const uint64_t sl = r.new_list[j];
-      r.tab.meta[8 * sl + 7] = fbase + rank + 1;
+      r.tab.ent[8 * (fbase + j) + 5] = base + v;  // first_seen, global record index
       r.tab.cmap[fbase + j] = (uint32_t)(fbase + rank);
       if (r.update_persist) r.tab.cnt[2 * (fbase + rank)] = r.tab.cnt[2 * (fbase + rank) + 1] = 0;
     }
@@ -912,7 +978,7 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
   }
   uint64_t wmax = 0;
   for (uint64_t j = tid; j < n_new; j += 1024) {
-    const uint64_t local = r.tab.meta[8 * r.new_list[j] + 6] - base;
+    const uint64_t local = new_flow_fs(r, j);
     if ((local >> 5) < r.nwords) {
       atomicOr(&r.bitmap[local >> 5], 1u << (local & 31));
       wmax = (local >> 5) > wmax ? (local >> 5) : wmax;
@@ -969,8 +1035,7 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
   }
   __syncthreads();
   for (uint64_t j = tid; j < n_new; j += 1024) {
-    const uint64_t s = r.new_list[j];
-    const uint64_t local = r.tab.meta[8 * s + 6] - base;
+    const uint64_t local = new_flow_fs(r, j);
     const uint64_t w = local >> 5;
     uint64_t id = fbase + n_new - 1;  // first_seen outside the batch (an invalid merge
                                       // input, flagged by its exporter): no bitmap read
@@ -979,7 +1044,7 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
                              ((1u << (local & 31)) - 1u);
       id = fbase + r.wprefix[w] + __popc(below);
     }
-    r.tab.meta[8 * s + 7] = id + 1;
+    r.tab.ent[8 * (fbase + j) + 5] = base + local;
     r.tab.cmap[fbase + j] = (uint32_t)id;
     if (r.update_persist) r.tab.cnt[2 * id] = r.tab.cnt[2 * id + 1] = 0;
   }
@@ -988,13 +1053,11 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
 
 __global__ __launch_bounds__(kBlock) void k_mark(RankArgs r) {
   __shared__ uint64_t s_wmax[kBlock / 64];
-  const uint64_t n_new = r.batch->n_new;
-  const uint64_t base = r.persist->rec_base;
+  const uint64_t n_new = rank_new(r, r.persist->flow_count);
   uint64_t wmax = 0;
   for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n_new;
        j += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t s = r.new_list[j];
-    const uint64_t local = r.tab.meta[8 * s + 6] - base;
+    const uint64_t local = new_flow_fs(r, j);
     if ((local >> 5) < r.nwords) {
       atomicOr(&r.bitmap[local >> 5], 1u << (local & 31));
       wmax = (local >> 5) > wmax ? (local >> 5) : wmax;
@@ -1072,9 +1135,10 @@ __global__ __launch_bounds__(kBlock) void k_scan_blocks(RankArgs r) {
     // launch and k_assign reads them). Round 2 had k_assign's last block do it:
     // one same-address device atomic per block cost ~10 us
     const uint64_t base = r.persist->rec_base, fbase = r.persist->flow_count;
-    const uint64_t n_new = r.batch->n_new;
+    const uint64_t n_new = rank_new(r, fbase);
     r.persist->rank_base = base;
     r.persist->rank_fbase = fbase;
+    r.batch->n_new = n_new;  // the claimed ones (k_assign and everything after)
     r.batch->flow_total = fbase + n_new;
     if (r.update_persist) {
       r.persist->rec_base = base + r.batch->n_acc;
@@ -1102,15 +1166,14 @@ __global__ void k_assign(RankArgs r) {
   const uint64_t fbase = r.persist->rank_fbase;
   for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n_new;
        j += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t s = r.new_list[j];
-    const uint64_t local = r.tab.meta[8 * s + 6] - base;
+    const uint64_t local = new_flow_fs(r, j);
     const uint64_t w = local >> 5;
     uint64_t id = fbase + n_new - 1;  // first_seen outside the batch: see k_rank_small
     if (w < lim) {
       const uint32_t below = r.bitmap[w] & ((1u << (local & 31)) - 1u);
       id = fbase + r.bprefix[w / kScanWordsPerBlock] + r.wprefix[w] + __popc(below);
     }
-    r.tab.meta[8 * s + 7] = id + 1;
+    r.tab.ent[8 * (fbase + j) + 5] = base + local;
     r.tab.cmap[fbase + j] = (uint32_t)id;
     if (r.update_persist) r.tab.cnt[2 * id] = r.tab.cnt[2 * id + 1] = 0;
   }
@@ -1782,6 +1845,145 @@ __global__ __launch_bounds__(BS) void k_count_chunk(CountArgs c) {
   }
 }
 
+// k_count_chunk in 76 KiB of LDS, so TWO workgroups share a CU and one's barrier
+// waits hide under the other's loads and gathers (round 3; k_count_chunk needs
+// 132 KiB and ran latency-bound at 2.5 TB/s, one workgroup per CU). Per chunk of
+// U * BS = 12288 records:
+//  s_rw[pos]  = claim | min(caplen, kLenSat) << 21 of the record at chunk position
+//               pos (claims < 510 * 4096 < 2^21 wherever the chunked mode runs;
+//               ~0 = no flow); after the gather, the record's output id
+//  s_pos[idx] = the chunk position of bucket-sorted entry idx (u16)
+// 6 B per record instead of 8. The sorted walk reads s_pos[idx] -> s_rw[pos], stores
+// the region entry at region[chunk + idx] and the id back into s_rw[pos] — a slot
+// only its own reader touches, so no barrier between the gather and the write-back.
+constexpr uint32_t kLenSat = 2047;  // caplens >= kLenSat are re-read from the K1 scratch
+template <bool PACK, int BS, int U>
+// (two workgroups of BS / 64 waves on a CU's 4 SIMDs: BS / 128 waves per SIMD)
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(BS / 128, 8)))
+void k_count_chunk2(CountArgs c) {
+  constexpr int CH = U * BS;
+  __shared__ uint32_t s_rw[CH];
+  __shared__ uint16_t s_pos[CH];
+  __shared__ uint32_t s_ch[kChunkMaxNb + 1], s_co[kChunkMaxNb + 1];
+  __shared__ uint32_t s_w[BS / 64];
+  static_assert(CH <= (1 << 16) && kChunkMaxNb < BS && (uint64_t)kChunkMaxNb * kBucket < (1u << 21),
+                "layout");
+  const uint64_t nflows = c.batch->flow_total;
+  if (count_mode(c, nflows) != 1 || !chunk_scatter(c, nflows) || c.chunk != (uint32_t)CH) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);  // spare bucket: nb
+  const uint64_t n_acc = c.batch->n_acc;
+  const uint64_t nchunks = (n_acc + CH - 1) / CH;
+  const uint32_t lmax = 0xFFFFFFFFu >> c.pack_bits;
+  for (uint32_t b = tid; b <= nb; b += BS) s_ch[b] = 0;
+  __syncthreads();
+  for (uint64_t q = blockIdx.x; q < nchunks; q += gridDim.x) {
+    const uint64_t base = q * CH;
+    const uint64_t hi = base + CH < n_acc ? base + CH : n_acc;
+    const uint32_t nval = (uint32_t)(hi - base);
+    uint32_t w[U], lp[U];
+    // chunk-relative 32-bit offsets from a uniform base: global loads with an SGPR
+    // base address (64-bit per-lane addresses cost the registers that let two
+    // workgroups share a CU)
+    const uint32_t* af = c.acc_flow + base;
+    const uint32_t* al = c.acc_len + base;
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint32_t pos = (uint32_t)k * BS + tid;
+      w[k] = __builtin_nontemporal_load(&af[pos < nval ? pos : 0u]);
+      if (!PACK) lp[k] = __builtin_nontemporal_load(&al[pos < nval ? pos : 0u]);  // (lp: len)
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint32_t pos = (uint32_t)k * BS + tid;
+      const uint32_t v = w[k];
+      uint32_t cl, len;
+      if (PACK) {
+        cl = v == 0xFFFFFFFFu ? v : (v & ((1u << c.pack_bits) - 1u));
+        len = v >> c.pack_bits;
+        if (len == lmax && cl != 0xFFFFFFFFu) len = al[pos];  // saturated: the side array
+      } else {
+        cl = v;
+        len = lp[k];
+      }
+      if (pos >= nval) cl = 0xFFFFFFFFu;
+      const bool big = len >= kRegLenEsc;
+      if (big && cl != 0xFFFFFFFFu)
+        atomicAdd((unsigned long long*)&c.cnt[2ull * c.cmap[cl] + 1], (unsigned long long)len);
+      const uint32_t l = big ? 0u : (len < kLenSat ? len : kLenSat);
+      w[k] = cl == 0xFFFFFFFFu ? 0xFFFFFFFFu : (cl | l << 21);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const bool valid = (uint32_t)k * BS + tid < nval;
+      const uint32_t bk = w[k] == 0xFFFFFFFFu ? nb : (w[k] & 0x1FFFFFu) >> kBucketBits;
+      const uint32_t b0 = __builtin_amdgcn_readfirstlane(bk);
+      const uint64_t vm = __ballot(valid);
+      if (__all(!valid || bk == b0)) {
+        // one add for the wave (a hot flow's bucket): ranks in lane order
+        uint32_t r0 = 0;
+        if (lane == 0 && vm) r0 = atomicAdd(&s_ch[b0], (uint32_t)__popcll(vm));
+        r0 = __shfl(r0, 0);
+        lp[k] = r0 + (uint32_t)__popcll(vm & lanemask_lt());
+      } else {
+        lp[k] = valid ? atomicAdd(&s_ch[bk], 1u) : 0u;
+      }
+    }
+    __syncthreads();
+    {
+      uint32_t tot;
+      const uint32_t off = block1024_excl_scan<BS>(tid <= nb ? s_ch[tid] : 0u, s_w, tot);
+      if (tid <= nb) s_co[tid] = off;
+      if (tid <= nb) c.coffs[q * (kChunkMaxNb + 1) + tid] = off;  // [nb] = end of the real buckets
+      if (tid <= nb) s_ch[tid] = 0;  // read by the scan only: zero for the next chunk
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint32_t pos = (uint32_t)k * BS + tid;
+      if (pos >= nval) continue;
+      const uint32_t bk = w[k] == 0xFFFFFFFFu ? nb : (w[k] & 0x1FFFFFu) >> kBucketBits;
+      s_pos[s_co[bk] + lp[k]] = (uint16_t)pos;
+      s_rw[pos] = w[k];
+    }
+    __syncthreads();
+    uint32_t* rg = c.region + base;
+#pragma unroll 6
+    for (int k = 0; k < U; ++k) {
+      const uint32_t idx = (uint32_t)k * BS + tid;
+      if (idx >= nval) continue;
+      const uint32_t pos = s_pos[idx];
+      const uint32_t x = s_rw[pos];
+      uint32_t id = 0xFFFFFFFFu;
+      const uint32_t cl = x & 0x1FFFFFu;
+      if (x != 0xFFFFFFFFu && (cl >> kBucketBits) < nb) {
+        uint32_t l = x >> 21;
+        if (l == kLenSat) {  // a caplen of >= 2047 B: the full value from the K1 scratch
+          if (PACK) {
+            l = af[pos] >> c.pack_bits;
+            if (l == lmax) l = al[pos];
+          } else {
+            l = al[pos];
+          }
+        }
+        rg[idx] = (cl & (kBucket - 1u)) | l << kBucketBits;  // coalesced runs
+        id = c.omap[cl];  // one bucket's 16 KiB window per wave: L1-local
+      }
+      s_rw[pos] = id;  // only this thread reads or writes slot pos in this phase
+    }
+    __syncthreads();
+    if (c.out_id && base < c.out_cap) {
+      uint32_t* oi = c.out_id + base;
+      const uint32_t lim = c.out_cap - base < nval ? (uint32_t)(c.out_cap - base) : nval;
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint32_t pos = (uint32_t)k * BS + tid;
+        if (pos < lim) __builtin_nontemporal_store(s_rw[pos], &oi[pos]);
+      }
+    }
+  }
+}
+
 // Mode 1, phase 2: workgroup (j, s) histograms bucket j over the segments of K3
 // blocks s, s+S, ... (S = gridDim / nb) in LDS; each wave walks one block's
 // segment at a time, 4 records per lane in flight. Writes a dense partial row.
@@ -1959,22 +2161,21 @@ __global__ void k_finalize(BatchState* b, PersistState* p, uint64_t out_cap, uin
 // ---------------------------------------------------------------------------
 __global__ void k_export(FlowTable t, uint64_t* out, uint64_t cap, const PersistState* p,
                          uint64_t* n_out) {
-  const uint64_t nslots = t.mask + 1;
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < nslots;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t* m = t.meta + 8 * s;
-    if (m[0] < 2 || m[7] == 0) continue;
-    const uint64_t id = m[7] - 1;
+  const uint64_t nflows = p->flow_count;
+  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nflows;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t* m = t.ent + 8 * c;  // key m[0..4], first_seen m[5]
+    const uint64_t id = t.cmap[c];
     if (id >= cap) continue;
     uint64_t* e = out + 8 * id;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) e[j] = m[1 + j];
+    for (int j = 0; j < 5; ++j) e[j] = m[j];
     e[5] = t.cnt[2 * id];
     e[6] = t.cnt[2 * id + 1];
-    e[7] = m[6];
+    e[7] = m[5];
   }
   if (n_out && blockIdx.x == 0 && threadIdx.x == 0) {
-    n_out[0] = p->flow_count < cap ? p->flow_count : cap;
+    n_out[0] = nflows < cap ? nflows : cap;
     n_out[1] = p->rec_base;  // accepted frames so far = records of this segment
   }
 }
@@ -1984,33 +2185,34 @@ __global__ void k_export(FlowTable t, uint64_t* out, uint64_t cap, const Persist
 // is mapped to its frame (rec_frame[r], or r itself when every frame of the batch
 // was accepted) and that frame to its position in the global trace. A first
 // record that cannot be placed flags kStShard and exports first_seen ~0.
+__device__ __forceinline__ uint64_t place_first(const GlobalExportArgs& g, uint64_t fs, uint64_t lo,
+                                                uint64_t hi, bool bad_batch) {
+  if (fs >= lo && fs < hi && fs - lo < g.out_cap && !bad_batch) {
+    const uint64_t r = fs - lo;
+    const uint64_t fr = g.rec_frame == nullptr ? r : g.rec_frame[r];
+    if (fr < g.n_frames) return g.frame_gidx[fr];
+  }
+  return ~0ull;
+}
+
 __global__ void k_export_global(GlobalExportArgs g) {
-  const uint64_t nslots = g.tab.mask + 1;
   const uint64_t nacc = g.batch->n_acc;
   const uint64_t lo = g.persist->rec_base - nacc;  // advanced by K2
   const uint64_t hi = lo + nacc;
   const uint64_t nflows = g.persist->flow_count;
-  const bool identity = g.rec_frame == nullptr;
-  const bool bad_batch = identity && nacc != g.n_frames;
+  const bool bad_batch = g.rec_frame == nullptr && nacc != g.n_frames;
   bool bad = false;
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < nslots;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t* m = g.tab.meta + 8 * s;
-    if (m[0] < 2 || m[7] == 0) continue;
-    const uint64_t id = m[7] - 1;
+  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nflows;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t* m = g.tab.ent + 8 * c;
+    const uint64_t id = g.tab.cmap[c];
     if (id >= g.cap) continue;
     uint64_t* e = g.out + 8 * id;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) e[j] = m[1 + j];
+    for (int j = 0; j < 5; ++j) e[j] = m[j];
     e[5] = g.tab.cnt[2 * id];
     e[6] = g.tab.cnt[2 * id + 1];
-    const uint64_t fs = m[6];
-    uint64_t gfs = ~0ull;
-    if (fs >= lo && fs < hi && fs - lo < g.out_cap && !bad_batch) {
-      const uint64_t r = fs - lo;
-      const uint64_t fr = identity ? r : g.rec_frame[r];
-      if (fr < g.n_frames) gfs = g.frame_gidx[fr];
-    }
+    const uint64_t gfs = place_first(g, m[5], lo, hi, bad_batch);
     bad = bad || gfs == ~0ull;
     e[7] = gfs;
   }
@@ -2024,18 +2226,16 @@ __global__ void k_export_global(GlobalExportArgs g) {
 
 // Records of this rank below each merged flow's first frame: a binary search
 // over the rank's record stream, whose global frame indices ascend.
-__global__ void k_records_before(FlowTable t, const uint32_t* rec_frame,
+__global__ void k_records_before(FlowTable t, const PersistState* p, const uint32_t* rec_frame,
                                  const uint64_t* frame_gidx, const uint64_t* n_rec_dev,
                                  uint64_t n_rec_max, uint64_t* out, uint64_t cap) {
-  const uint64_t nslots = t.mask + 1;
+  const uint64_t nflows = p->flow_count;
   const uint64_t n = n_rec_dev && *n_rec_dev < n_rec_max ? *n_rec_dev : n_rec_max;
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < nslots;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t* m = t.meta + 8 * s;
-    if (m[0] < 2 || m[7] == 0) continue;
-    const uint64_t id = m[7] - 1;
+  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nflows;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t id = t.cmap[c];
     if (id >= cap) continue;
-    const uint64_t G = m[6];
+    const uint64_t G = t.ent[8 * c + 5];
     uint64_t lo = 0, len = n;  // first record whose global frame >= G
     while (len > 0) {
       const uint64_t half = len >> 1, mid = lo + half;
@@ -2051,14 +2251,13 @@ __global__ void k_records_before(FlowTable t, const uint32_t* rec_frame,
   }
 }
 
-__global__ void k_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t cap) {
-  const uint64_t nslots = t.mask + 1;
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < nslots;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t* m = t.meta + 8 * s;
-    if (m[0] < 2 || m[7] == 0) continue;
-    const uint64_t id = m[7] - 1;
-    if (id < cap) m[6] = fs_by_id[id];
+__global__ void k_set_first_seen(FlowTable t, const PersistState* p, const uint64_t* fs_by_id,
+                                 uint64_t cap) {
+  const uint64_t nflows = p->flow_count;
+  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nflows;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t id = t.cmap[c];
+    if (id < cap) t.ent[8 * c + 5] = fs_by_id[id];
   }
 }
 
@@ -2067,30 +2266,21 @@ __global__ void k_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t
 // each one's first record (placed as k_export_global places it) at out[id - fbase];
 // n_out = {n_new, fbase}. Batches are windows of one global trace (the same global
 // frame range on every rank), so the flows new in a window are exactly the union
-// of every rank's new flows, and older flows keep the ids they already have.
+// of every rank's new flows, and older flows keep the ids they already have. The
+// batch's new flows are its claims [fbase, fbase + n_new) (ids a permutation of them).
 __global__ void k_first_frames(GlobalExportArgs g) {
-  const uint64_t nslots = g.tab.mask + 1;
   const uint64_t nacc = g.batch->n_acc;
   const uint64_t lo = g.persist->rec_base - nacc;  // advanced by K2
   const uint64_t hi = lo + nacc;
   const uint64_t nnew = g.batch->n_new;
   const uint64_t fbase = g.persist->flow_count - nnew;
-  const bool identity = g.rec_frame == nullptr;
-  const bool bad_batch = identity && nacc != g.n_frames;
+  const bool bad_batch = g.rec_frame == nullptr && nacc != g.n_frames;
   bool bad = false;
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < nslots;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t* m = g.tab.meta + 8 * s;
-    if (m[0] < 2 || m[7] == 0) continue;
-    const uint64_t id = m[7] - 1;
+  for (uint64_t c = fbase + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < fbase + nnew;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t id = g.tab.cmap[c];
     if (id < fbase || id - fbase >= g.cap) continue;
-    const uint64_t fs = m[6];
-    uint64_t gfs = ~0ull;
-    if (fs >= lo && fs < hi && fs - lo < g.out_cap && !bad_batch) {
-      const uint64_t r = fs - lo;
-      const uint64_t fr = identity ? r : g.rec_frame[r];
-      if (fr < g.n_frames) gfs = g.frame_gidx[fr];
-    }
+    const uint64_t gfs = place_first(g, g.tab.ent[8 * c + 5], lo, hi, bad_batch);
     bad = bad || gfs == ~0ull;
     g.out[id - fbase] = gfs;
   }
@@ -2154,7 +2344,7 @@ __global__ __launch_bounds__(kBlock) void k_owner_bucket(OwnerArgs a) {
   __shared__ uint32_t s_cnt[kMaxOwners];
   __shared__ uint64_t s_base[kMaxOwners];
   const uint32_t tid = threadIdx.x;
-  const uint64_t nslots = a.tab.mask + 1;
+  const uint64_t nflows = a.persist->flow_count;
   if (tid < a.world) s_cnt[tid] = 0;
   if (blockIdx.x == 0 && tid == 0) a.meta[a.world] = a.persist->rec_base;
   __syncthreads();
@@ -2164,17 +2354,16 @@ __global__ __launch_bounds__(kBlock) void k_owner_bucket(OwnerArgs a) {
 #pragma unroll
   for (int k = 0; k < kOwnerItems; ++k) {
     own[k] = 0xFFFFFFFFu;
-    const uint64_t s = s0 + (uint64_t)k * kBlock;
-    if (s >= nslots) continue;
-    const uint64_t* m = a.tab.meta + 8 * s;
-    if (m[0] < 2 || m[7] == 0) continue;
+    const uint64_t c = s0 + (uint64_t)k * kBlock;  // claim
+    if (c >= nflows) continue;
+    const uint64_t* m = a.tab.ent + 8 * c;
     // a flow whose local id has no place in the id map takes NO segment slot (a
     // counted but unwritten slot would reach its owner as a phantom flow)
-    if (m[7] - 1 >= a.map_cap) {
+    if (a.tab.cmap[c] >= a.map_cap) {
       ++dropped;
       continue;
     }
-    own[k] = fold32(flow_hash64(m[1], m[2], m[3], m[4], m[5])) % a.world;
+    own[k] = fold32(flow_hash64(m[0], m[1], m[2], m[3], m[4])) % a.world;
     rank[k] = atomicAdd(&s_cnt[own[k]], 1u);
   }
   __syncthreads();
@@ -2187,8 +2376,8 @@ __global__ __launch_bounds__(kBlock) void k_owner_bucket(OwnerArgs a) {
   for (int k = 0; k < kOwnerItems; ++k) {
     if (own[k] == 0xFFFFFFFFu) continue;
     const uint64_t pos = s_base[own[k]] + rank[k];
-    const uint64_t s = s0 + (uint64_t)k * kBlock;
-    const uint64_t* m = a.tab.meta + 8 * s;
+    const uint64_t c = s0 + (uint64_t)k * kBlock;
+    const uint64_t* m = a.tab.ent + 8 * c;
     if (pos >= a.seg_cap) {  // positions [0, seg_cap) of every segment stay dense
       ++dropped;
       continue;
@@ -2196,11 +2385,11 @@ __global__ __launch_bounds__(kBlock) void k_owner_bucket(OwnerArgs a) {
     const uint64_t e = (uint64_t)own[k] * a.seg_cap + pos;
     uint64_t* out = a.ent + 8 * e;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) out[j] = m[1 + j];
+    for (int j = 0; j < 5; ++j) out[j] = m[j];
     out[5] = 0;  // pkts / bytes: K3 has not run (the ids come first)
     out[6] = 0;
-    out[7] = m[6];  // first_seen, local to this rank's record stream
-    a.lid[e] = (uint32_t)(m[7] - 1);
+    out[7] = m[5];  // first_seen, local to this rank's record stream
+    a.lid[e] = a.tab.cmap[c];
   }
   // meta[world + 1]: entries this rank dropped. Every rank sees it after the meta
   // all-gather, so the PEERS of an overflowing rank can flag their ids as wrong too
@@ -2222,13 +2411,11 @@ __global__ void k_status_raise(const uint64_t* v, uint64_t n, uint64_t stride, u
 
 __global__ void k_first_seen(FlowTable t, const PersistState* p, uint64_t* out, uint64_t cap,
                              uint64_t* n_out) {
-  const uint64_t nslots = t.mask + 1;
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < nslots;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t* m = t.meta + 8 * s;
-    if (m[0] < 2 || m[7] == 0) continue;
-    const uint64_t id = m[7] - 1;
-    if (id < cap) out[id] = m[6];
+  const uint64_t nflows = p->flow_count;
+  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nflows;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t id = t.cmap[c];
+    if (id < cap) out[id] = t.ent[8 * c + 5];
   }
   if (n_out && blockIdx.x == 0 && threadIdx.x == 0) {
     n_out[0] = p->flow_count < cap ? p->flow_count : cap;
@@ -2286,36 +2473,37 @@ __global__ void k_merge_insert(MergeArgs g) {
     }
     const uint64_t* E = g.ent + 8 * e;
     const uint64_t K[5] = {E[0], E[1], E[2], E[3], E[4]};
-    uint64_t fs = ~0ull;
-    uint32_t claim;
+    uint32_t fs = 0xFFFFFFFFu, claim = 0xFFFFFFFFu;
+    // (a fresh table: every claim is new, fbase 0)
     const uint32_t s = flow_upsert(g.tab, K, flow_hash64(K[0], K[1], K[2], K[3], K[4]), g.batch,
-                                   g.new_list, g.persist, fs, claim);
-    g.out_slot[e] = s;
+                                   g.new_list, g.persist, 0, fs, claim);
+    g.out_slot[e] = s == 0xFFFFFFFFu ? 0xFFFFFFFFu : claim;
     if (s == 0xFFFFFFFFu) continue;
-    atomicAdd((unsigned long long*)&g.mcnt[2ull * s], (unsigned long long)E[5]);
-    atomicAdd((unsigned long long*)&g.mcnt[2ull * s + 1], (unsigned long long)E[6]);
+    atomicAdd((unsigned long long*)&g.mcnt[2ull * claim], (unsigned long long)E[5]);
+    atomicAdd((unsigned long long*)&g.mcnt[2ull * claim + 1], (unsigned long long)E[6]);
     uint64_t base = 0;  // records of the segments before this one
     for (uint64_t q = 0; q < seg; ++q) base += g.seg_meta[2 * q + 1];
-    atomicMin((unsigned long long*)&g.tab.meta[8ull * s + 6], (unsigned long long)(base + E[7]));
+    // the slot's fs32 (max_total_records < 2^31, checked by the ABI); an unplaceable
+    // first_seen (~0 from a flagged exporter) stays past every record of the merge
+    const uint64_t gfs = base + E[7];
+    atomicMin(slot_fs(g.tab, s), gfs < (uint64_t)kFs32Flag ? (uint32_t)gfs : kFs32Flag - 1u);
   }
 }
 
 // entry slot -> merged dense id; per-slot counters -> by-id counters; flow count
 __global__ void k_merge_finish(MergeArgs g) {
   const uint64_t total = g.nseg * g.stride;
-  const uint64_t nslots = g.tab.mask + 1;
+  const uint64_t nflows = g.batch->n_new;  // a fresh table: claims [0, n_new)
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   for (uint64_t e = t0; e < total; e += stride) {
-    const uint32_t s = g.out_slot[e];
-    g.out_slot[e] = s == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)(g.tab.meta[8ull * s + 7] - 1);
+    const uint32_t c = g.out_slot[e];
+    g.out_slot[e] = c == 0xFFFFFFFFu || c >= nflows ? 0xFFFFFFFFu : g.tab.cmap[c];
   }
-  for (uint64_t s = t0; s < nslots; s += stride) {
-    const uint64_t* m = g.tab.meta + 8 * s;
-    if (m[0] < 2 || m[7] == 0) continue;
-    const uint64_t id = m[7] - 1;
-    g.tab.cnt[2 * id] = g.mcnt[2 * s];
-    g.tab.cnt[2 * id + 1] = g.mcnt[2 * s + 1];
+  for (uint64_t c = t0; c < nflows; c += stride) {
+    const uint64_t id = g.tab.cmap[c];
+    g.tab.cnt[2 * id] = g.mcnt[2 * c];
+    g.tab.cnt[2 * id + 1] = g.mcnt[2 * c + 1];
   }
   for (uint64_t w = t0; w <= g.batch->fs_max_word; w += stride) g.bitmap[w] = 0;
   if (t0 == 0) {
@@ -2491,7 +2679,7 @@ static unsigned grid_for(uint64_t n, unsigned cap = 4096) {
 }
 
 hipError_t launch_table_init(FlowTable t, hipStream_t s) {
-  hipLaunchKernelGGL(k_table_init, dim3(grid_for(t.mask + 1)), dim3(kBlock), 0, s, t);
+  hipLaunchKernelGGL(k_table_init, dim3(grid_for(8 * t.nlines)), dim3(kBlock), 0, s, t);
   return hipGetLastError();
 }
 
@@ -2577,7 +2765,7 @@ hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s, 
 
 hipError_t launch_prep(const PrepArgs& p, hipStream_t s) {
   uint64_t work = p.ntiles;
-  if (p.reset && p.tab.mask + 1 > work) work = p.tab.mask + 1;
+  if (p.reset && 8 * p.tab.nlines > work) work = 8 * p.tab.nlines;
   hipLaunchKernelGGL(k_prep, dim3(grid_for(work < 4 ? 4 : work)), dim3(kBlock), 0, s, p);
   return hipGetLastError();
 }
@@ -2638,7 +2826,19 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
     else hipLaunchKernelGGL((k_count_scatter_staged<4, false>), gs, dim3(kCountBlock), 0, s, c);
   }
   if (g2) {
-    if (c.coffs && c.chunk == 16u * 1024u) {  // 132 KiB of LDS: one workgroup per CU
+    if (c.coffs && c.chunk == 12u * 1024u) {  // 76 KiB of LDS: two workgroups per CU
+      const dim3 gc(g1s ? g1s : 1);
+      // 512-thread workgroups, 24 records per thread (TCBEE_K3ABL=94: 1024 x 12, A/B):
+      // 125M records, 125k flows (packed words): 470 vs 476 us; 1M flows (unpacked):
+      // 705 vs 827 us (round 2's k_count_chunk: 607 / 868 us; profiles/r03_k3ab_*)
+      if (k3v == 94) {
+        if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk2<true, 1024, 12>), gc, dim3(1024), 0, s, c);
+        else hipLaunchKernelGGL((k_count_chunk2<false, 1024, 12>), gc, dim3(1024), 0, s, c);
+      } else {
+        if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk2<true, 512, 24>), gc, dim3(512), 0, s, c);
+        else hipLaunchKernelGGL((k_count_chunk2<false, 512, 24>), gc, dim3(512), 0, s, c);
+      }
+    } else if (c.coffs && c.chunk == 16u * 1024u) {  // 132 KiB of LDS: one workgroup per CU
       const dim3 gc((g1s + 1) / 2);
       if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk<true, 1024>), gc, dim3(1024), 0, s, c);
       else hipLaunchKernelGGL((k_count_chunk<false, 1024>), gc, dim3(1024), 0, s, c);
@@ -2664,31 +2864,33 @@ hipError_t launch_finalize(BatchState* b, PersistState* p, uint64_t out_cap, uin
 
 hipError_t launch_export(FlowTable t, uint64_t* out, uint64_t cap, const PersistState* p,
                          uint64_t* n_out, hipStream_t s) {
-  hipLaunchKernelGGL(k_export, dim3(grid_for(t.mask + 1)), dim3(kBlock), 0, s, t, out, cap, p, n_out);
+  hipLaunchKernelGGL(k_export, dim3(grid_for(t.max_claims)), dim3(kBlock), 0, s, t, out, cap, p, n_out);
   return hipGetLastError();
 }
 
 hipError_t launch_export_global(const GlobalExportArgs& g, hipStream_t s) {
-  hipLaunchKernelGGL(k_export_global, dim3(grid_for(g.tab.mask + 1)), dim3(kBlock), 0, s, g);
+  hipLaunchKernelGGL(k_export_global, dim3(grid_for(g.tab.max_claims)), dim3(kBlock), 0, s, g);
   return hipGetLastError();
 }
 
-hipError_t launch_records_before(FlowTable t, const uint32_t* rec_frame, const uint64_t* frame_gidx,
-                                 const uint64_t* n_rec, uint64_t n_rec_max, uint64_t* out,
+hipError_t launch_records_before(FlowTable t, const PersistState* p, const uint32_t* rec_frame,
+                                 const uint64_t* frame_gidx, const uint64_t* n_rec,
+                                 uint64_t n_rec_max, uint64_t* out, uint64_t cap, hipStream_t s) {
+  hipLaunchKernelGGL(k_records_before, dim3(grid_for(t.max_claims)), dim3(kBlock), 0, s, t, p,
+                     rec_frame, frame_gidx, n_rec, n_rec_max, out, cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_set_first_seen(FlowTable t, const PersistState* p, const uint64_t* fs_by_id,
                                  uint64_t cap, hipStream_t s) {
-  hipLaunchKernelGGL(k_records_before, dim3(grid_for(t.mask + 1)), dim3(kBlock), 0, s, t, rec_frame,
-                     frame_gidx, n_rec, n_rec_max, out, cap);
-  return hipGetLastError();
-}
-
-hipError_t launch_set_first_seen(FlowTable t, const uint64_t* fs_by_id, uint64_t cap, hipStream_t s) {
-  hipLaunchKernelGGL(k_set_first_seen, dim3(grid_for(t.mask + 1)), dim3(kBlock), 0, s, t, fs_by_id, cap);
+  hipLaunchKernelGGL(k_set_first_seen, dim3(grid_for(t.max_claims)), dim3(kBlock), 0, s, t, p,
+                     fs_by_id, cap);
   return hipGetLastError();
 }
 
 hipError_t launch_owner_bucket(const OwnerArgs& a, hipStream_t s) {
   const uint64_t per = (uint64_t)kBlock * kOwnerItems;
-  const uint64_t nb = (a.tab.mask + 1 + per - 1) / per;
+  const uint64_t nb = (a.tab.max_claims + per - 1) / per;
   hipLaunchKernelGGL(k_owner_bucket, dim3((unsigned)nb), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
@@ -2701,7 +2903,7 @@ hipError_t launch_status_raise(const uint64_t* v, uint64_t n, uint64_t stride, u
 
 hipError_t launch_first_seen(FlowTable t, const PersistState* p, uint64_t* out, uint64_t cap,
                              uint64_t* n_out, hipStream_t s) {
-  hipLaunchKernelGGL(k_first_seen, dim3(grid_for(t.mask + 1)), dim3(kBlock), 0, s, t, p, out, cap,
+  hipLaunchKernelGGL(k_first_seen, dim3(grid_for(t.max_claims)), dim3(kBlock), 0, s, t, p, out, cap,
                      n_out);
   return hipGetLastError();
 }
@@ -2723,7 +2925,7 @@ hipError_t launch_owner_apply(const uint32_t* back, const uint32_t* lid, const u
 }
 
 hipError_t launch_first_frames(const GlobalExportArgs& g, hipStream_t s) {
-  hipLaunchKernelGGL(k_first_frames, dim3(grid_for(g.tab.mask + 1)), dim3(kBlock), 0, s, g);
+  hipLaunchKernelGGL(k_first_frames, dim3(grid_for(g.tab.max_claims)), dim3(kBlock), 0, s, g);
   return hipGetLastError();
 }
 
@@ -2748,7 +2950,7 @@ hipError_t launch_merge(const MergeArgs& g, const RankArgs& r, hipStream_t s) {
   hipLaunchKernelGGL(k_merge_insert, dim3(grid), dim3(kBlock), 0, s, g);
   hipError_t e = launch_rank(r, s);
   if (e != hipSuccess) return e;
-  const uint64_t work = g.nseg * g.stride > g.tab.mask + 1 ? g.nseg * g.stride : g.tab.mask + 1;
+  const uint64_t work = g.nseg * g.stride > g.tab.max_claims ? g.nseg * g.stride : g.tab.max_claims;
   hipLaunchKernelGGL(k_merge_finish, dim3(grid_for(work)), dim3(kBlock), 0, s, g);
   return hipGetLastError();
 }

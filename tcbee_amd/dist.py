@@ -382,8 +382,11 @@ class OwnerExchange:
 
     def merged_flows(self, merged: "_parser.PacketParser", n_dev, n_max: int):
         """The global flow table on every rank (collective): the all-gather merge of
-        FlowMerge, once, on request."""
-        fm = FlowMerge(self.local, merged, self.map_cap, self.max_total, self.group)
+        FlowMerge, once, on request. The ranks' map_cap may differ; the all-gather
+        takes the largest (its segments must be the same size everywhere)."""
+        cap = torch.tensor([self.map_cap], dtype=torch.int64, device=self.gmap.device)
+        dist.all_reduce(cap, op=dist.ReduceOp.MAX, group=self.group)
+        fm = FlowMerge(self.local, merged, int(cap.item()), self.max_total, self.group)
         s = torch.cuda.current_stream().cuda_stream
         fm.step(None, n_dev, n_max, stream=s)
         torch.cuda.synchronize()

@@ -278,15 +278,16 @@ def test_gpu_owner_exchange_contiguous_real_trace(gpu, oracle, tmp_path, world, 
 
 
 def test_gpu_owner_exchange_map_overflow_is_refused(gpu, tmp_path):
-    """A rank with more flows than the id map holds: the flows past it are not
-    exchanged and the local context reports TCBEE_ESHARD (no silent garbage ids)."""
+    """Ranks with more flows than their id maps hold (~5.5k local flows each, maps of
+    4096): the flows past the map are not exchanged and every context reports
+    TCBEE_ESHARD (no silent garbage ids)."""
     import torch.multiprocessing as mp
 
     import dist_worker
     from tcbee_amd import _lib
-    n, flows, cap, world = 90_000, 3000, 4096, 2
+    n, flows, cap, world = 90_000, 3000, 8192, 2
     mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path), "owner",
-                                        flows), nprocs=world, join=True)
+                                        flows, 0, "gloo", [4096, 4096]), nprocs=world, join=True)
     for r in range(world):
         assert int(np.load(tmp_path / f"rank{r}.npz")["status"][0]) == _lib.ESHARD
 

@@ -313,7 +313,8 @@ def test_device_merge_matches_unsharded(gpu, oracle, cuts):
     cap, world = 2048, len(cuts) - 1
     ents, metas, ids = [], [], []
     for lo, hi in zip(cuts, cuts[1:]):
-        with tcbee_amd.PacketParser(max_frames=1 << 16, max_arena=1 << 24, max_flows=1024) as p:
+        # (~1.7k distinct keys: a mixed trace draws ~1.9 keys per pool flow)
+        with tcbee_amd.PacketParser(max_frames=1 << 16, max_arena=1 << 24, max_flows=cap) as p:
             res = p.parse(tr.slice(lo, hi))
             ent = torch.zeros((cap, 8), dtype=torch.int64, device="cuda")
             meta = torch.zeros(2, dtype=torch.int64, device="cuda")
@@ -418,8 +419,9 @@ def test_config4_scale_over_1M_flows_mixed(gpu, oracle):
     tr = mixed_trace(5_000_000, seed=4004, n_flows=1_700_000)
     cut = 2_500_000
     a, b = tr.slice(0, cut), tr.slice(cut, tr.n)
+    # (1.88M distinct keys: a mixed trace draws ~1.1 keys per pool flow at this size)
     with tcbee_amd.PacketParser(max_frames=cut, max_arena=max(len(a.arena), len(b.arena)),
-                                max_flows=1_600_000) as p:
+                                max_flows=2_000_000) as p:
         r1 = p.parse(a)
         r2 = p.parse(b)
         ft = oracle.new_flowtab(1 << 22)
@@ -440,8 +442,8 @@ def test_config4_scale_over_1M_flows_mixed(gpu, oracle):
 @pytest.mark.parametrize("cap_mult", [1, 4])
 def test_config4_1M_flows_device_right_sized(gpu, oracle, cap_mult):
     """1M synthetic IMIX flows, device-resident path; the table sized exactly for 1M
-    flows (max_flows = flows: 2^21 slots = 128 MiB, load 1/2) and at what bench.py
-    allocates for config 4 (max_flows = 4 x flows: 2^23 slots, load 1/8)."""
+    flows (max_flows = flows: every claim used, slot load 1/2, 43 MB of slot lines)
+    and 4x that (load 1/8)."""
     import torch
     n, flows = 3_500_000, 1_000_000
     tr = tcbee_amd.synth_trace(n, sizes="imix", kind=1, n_flows=flows)
@@ -582,19 +584,22 @@ def _concat(a, b):
                  np.concatenate([a.caplen, b.caplen]), np.concatenate([a.ts_ns, b.ts_ns]))
 
 
-@pytest.mark.parametrize("variant", ["0", "91", "92"])
+@pytest.mark.parametrize("variant", ["0", "0n", "94", "93", "91", "92"])
 @pytest.mark.parametrize("flows", [40_000, 150_000])
 def test_k3_chunked_scatter(gpu, oracle, variant, flows, monkeypatch):
-    """K3 mode 1's single-pass chunked scatter (k_count_chunk: chunks of 16384
-    records — 8192 with TCBEE_K3ABL=92 — bucket-sorted in LDS, ids gathered bucket
-    by bucket, region runs per chunk) and the two-pass scatter it replaced
-    (TCBEE_K3ABL=91), bit-exact vs the
+    """K3 mode 1's single-pass chunked scatter (k_count_chunk2: chunks of 12288
+    records in 76 KiB of LDS, two workgroups per CU — "0n": unpacked K1 -> K3
+    words, 94: 1024-thread workgroups of 12 records each; 93: round 2's k_count_chunk, 16384 records,
+    92: 8192 — bucket-sorted in LDS, ids gathered bucket by bucket, region runs per
+    chunk) and the two-pass scatter it replaced (TCBEE_K3ABL=91), bit-exact vs the
     oracle: a ragged last chunk, caplens past the 20-bit region field and the
     packed K1 -> K3 field, a single-flow stretch (every wave on one bucket), two
     batches (claims of batch 1 looked up again in batch 2)."""
     from tracegen import mixed_trace
     monkeypatch.setenv("TCBEE_TEST_K3_NORANGE", "1")
-    monkeypatch.setenv("TCBEE_K3ABL", variant)
+    monkeypatch.setenv("TCBEE_K3ABL", variant.rstrip("n"))
+    if variant.endswith("n"):
+        monkeypatch.setenv("TCBEE_TEST_NOPACK", "1")
     mt = mixed_trace(350_001, seed=123, n_flows=flows)
     rng = np.random.default_rng(9)
     big = rng.choice(mt.n, size=200, replace=False)

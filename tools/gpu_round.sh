@@ -47,6 +47,7 @@ for s in "$@"; do
     xprof)  step xprof 600 env MASTER_ADDR=127.0.0.1 MASTER_PORT=29543 RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 TCBEE_BENCH_FORCE_MERGE=1 rocprofv3 --kernel-trace --stats -d gpurun_out/xprof -o run --output-format csv -- python bench.py --config4 --steps 5 --warmup 1 --no-cpu --no-extra --sample-check ;;
     sq)     step sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS --output-format csv -d gpurun_out/sq -o run -- python tools/k1_sweep.py --rounds 1 --iters 2 --fpl 2 --workloads imix10k ;;
     prof)   step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --no-cpu --no-extra --sample-check ;;
+    c4fprof) step c4fprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/c4fprof -o run --output-format csv -- python bench.py --config4 --shard contig --steps 5 --warmup 1 --no-cpu --no-extra --sample-check ;;
     c4prof) step c4prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/c4prof -o run --output-format csv -- python bench.py --config4 --virtual-world 8 --steps 5 --warmup 1 --no-cpu --no-extra --sample-check ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
