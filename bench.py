@@ -157,10 +157,10 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     flows_here = -(-n_flows // sw) if flowhash else n_flows
     # table: max_flows = the shard's expected flows + 3 % + 64 (a flow-hash shard of
     # config 3 at N=8 holds up to +3 % of the mean; claims past max_flows are
-    # refused). The compact table (round 3) keeps >= 2 slots per max_flow (load
-    # <= 1/2), 6 slots per 128-B line, so one probe is one line of a table of ~43 B
-    # per flow: 43 MB at 1M flows, resident in the Infinity Cache beside the stream
-    # (rounds 1-2: 64-B slots at max_flows = 4x flows, 512 MiB at 1M flows)
+    # refused). The compact table (round 3) keeps 8 slots per max_flow (load <=
+    # 1/8), 6 slots per 128-B line: 176 MB at 1M flows (rounds 1-2: 64-B slots at
+    # max_flows = 4x flows, 512 MiB), and a tight max_flows keeps the K1 -> K3 word
+    # packed (claim | caplen) up to 2^20 flows
     cap = max(flows_here + flows_here // 32 + 64, 64)
     # (the exchange carries up to xcap entries per rank: a quarter more than the
     # shard's expected flows)

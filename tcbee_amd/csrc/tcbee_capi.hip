@@ -187,6 +187,8 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   dfree(c->tab.slots);
   dfree(c->tab.ent);
+  dfree(c->tab.wide);
+  dfree(c->tab.wide_used);
   dfree(c->tab.cnt);
   dfree(c->tab.cmap);
   dfree(c->d_persist);
@@ -268,8 +270,8 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   if (hipSetDevice(device) != hipSuccess) return fail(TCBEE_EDEVICE);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return fail(TCBEE_EDEVICE);
-  // slots >= 2 x max_flows (load <= 1/2), 6 per 128-B line
-  c->nlines = (2 * c->max_flows + kSlotsPerLine - 1) / kSlotsPerLine;
+  // kSlotsPerFlow x max_flows slots (load <= 1/8), 6 per 128-B line
+  c->nlines = (kSlotsPerFlow * c->max_flows + kSlotsPerLine - 1) / kSlotsPerLine;
   c->tab.nlines = c->nlines;
   c->tab.max_claims = c->max_flows;
   {
@@ -288,6 +290,15 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   hipError_t e = hipSuccess;
   if ((e = dalloc(&c->tab.slots, 16 * c->nlines)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.ent, 8 * c->max_flows)) != hipSuccess) return fail(map_err(e));
+  // wide slots (non-IPv4-form keys): a power of two >= kSlotsPerFlow x max_flows,
+  // at most 2^25 (2 GiB: K1's probe buffer resource and u32 offsets)
+  c->tab.wide_mask = 63;
+  while (c->tab.wide_mask + 1 < kSlotsPerFlow * c->max_flows && c->tab.wide_mask + 1 < (1ull << 25))
+    c->tab.wide_mask = 2 * c->tab.wide_mask + 1;
+  if ((e = dalloc(&c->tab.wide, 8 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
+  if ((e = hipMemset(c->tab.wide, 0, 64 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->tab.wide_used, 1)) != hipSuccess) return fail(map_err(e));
+  if ((e = hipMemset(c->tab.wide_used, 0, 4)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.cnt, 2 * c->max_flows)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.cmap, c->max_flows)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_persist, 1)) != hipSuccess) return fail(map_err(e));

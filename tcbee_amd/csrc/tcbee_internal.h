@@ -24,15 +24,19 @@ constexpr uint32_t kStFlowFull = 1u, kStSpin = 2u, kStShard = 4u;
 //      kind 2: an IPv4-form key (12 zero bytes + the address, xdp.rs:116-119):
 //              w0 = saddr | daddr << 32 (wire bytes), lo32 = sport | dport << 16 —
 //              the slot holds the whole key, so the slot alone decides a match
-//      kind 3: any other key: w0 = flow_hash64, lo32 = 0; the key is ent[claim]
+//      kind 3: (not used: other keys live in the wide slots below)
 //      kind 4/5: dead (2/3 refused because the table was full): the key's w0 and
 //              lo32, no claim — the flow's later frames find it and stay unclassified
 //    bytes 96 + 4*pos: fs32 of slot pos: the batch-local first record index of a
 //      flow new in this batch (kFs32Flag | frame while only its claimer's mark is
 //      known); stale for flows of earlier batches (never read for them)
-//    One probe = one line (16-B slot + its fs32): ~43 B of table per flow at load
-//    1/2 instead of the 64-B slots of rounds 1-2 (512 MiB at 1M flows, which no
-//    cache kept; 43 MB stays in the 256 MiB Infinity Cache beside the stream).
+//    One probe = one line (16-B slot + its fs32). kSlotsPerFlow slots per max_flow
+//    (load <= 1/8): ~171 B of slot lines per max_flow, 176 MB at 1M flows (rounds
+//    1-2: 64-B slots, 2-16 per max_flow, 512 MiB at bench's 1M flows). Measured
+//    (round 3, 125M IMIX frames, K1): load 1/2 costs 27 % at 10k flows and 29 % at
+//    1M (the linear-probe walks are dependent round trips); at equal load the
+//    compact lines match the 64-B slots (the cost of a large table is the probe's
+//    latency, not its bytes: a 44 MB table at load 1/2 was slower than 176 MB at 1/8).
 //  ent [claim*8 + 0..4] the 40-B key as 5 LE u64 words; [claim*8 + 5] first_seen
 //      (global accepted-record index, written by K2); 6..7 spare
 //  cnt [id*2 + 0/1]    pkts / bytes of dense flow id `id`
@@ -40,12 +44,24 @@ struct FlowTable {
   uint64_t* slots;
   uint64_t nlines;
   uint64_t* ent;
+  // wide slots (64 B, rounds 1-2's layout) for keys that are not IPv4-form: the
+  // 40-B key lives in the slot, so an IPv6 probe is one line and compares at once
+  // (a compact kind-3 slot + its entry cost K1 15 % on an all-IPv6 trace: a
+  // dependent load per frame). wide[s*8 + 0] tag word: 0 empty, 1 busy, else
+  // hash_tag32 | claim << 32 (claim ~0: dead, the table was full); [1..5] key;
+  // [6] low 32 bits: fs32 as the compact slots'
+  uint64_t* wide;
+  uint64_t wide_mask;    // wide slots - 1 (>= kSlotsPerFlow x max_flows, a power of 2)
+  uint32_t* wide_used;   // != 0 once a wide slot was claimed: resets sweep the wide
+                         // slots only then (an IPv4 capture never touches them)
   uint64_t* cnt;
   uint32_t* cmap;        // claim index -> dense id (0-based), written by K2; dense in
                          // [0, flows), so K3 stages it in LDS
   uint64_t max_claims;   // claims at or past it are refused (TCBEE_EFLOWFULL)
 };
 constexpr uint32_t kSlotsPerLine = 6;
+constexpr uint32_t kWideSlot = 1u << 31;  // slot ids: compact s, or wide s | kWideSlot
+constexpr uint64_t kSlotsPerFlow = 8;  // slots per max_flow: linear-probe load <= 1/8
 constexpr uint32_t kFs32Flag = 1u << 31;
 
 // Lives across batches of one context.

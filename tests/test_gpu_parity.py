@@ -442,8 +442,8 @@ def test_config4_scale_over_1M_flows_mixed(gpu, oracle):
 @pytest.mark.parametrize("cap_mult", [1, 4])
 def test_config4_1M_flows_device_right_sized(gpu, oracle, cap_mult):
     """1M synthetic IMIX flows, device-resident path; the table sized exactly for 1M
-    flows (max_flows = flows: every claim used, slot load 1/2, 43 MB of slot lines)
-    and 4x that (load 1/8)."""
+    flows (max_flows = flows: every claim used, slot load 1/8, 176 MB of slot lines)
+    and 4x that (load 1/32)."""
     import torch
     n, flows = 3_500_000, 1_000_000
     tr = tcbee_amd.synth_trace(n, sizes="imix", kind=1, n_flows=flows)
