@@ -270,7 +270,7 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   if (hipSetDevice(device) != hipSuccess) return fail(TCBEE_EDEVICE);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return fail(TCBEE_EDEVICE);
-  // kSlotsPerFlow x max_flows slots (load <= 1/8), 6 per 128-B line
+  // kSlotsPerFlow x max_flows slots (load <= 1/8), 3 per 64-B unit
   c->nlines = (kSlotsPerFlow * c->max_flows + kSlotsPerLine - 1) / kSlotsPerLine;
   c->tab.nlines = c->nlines;
   c->tab.max_claims = c->max_flows;
@@ -288,7 +288,7 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   c->max_words = (max_frames + 31) / 32;
   c->max_sblocks = (c->max_words + kScanWordsPerBlock - 1) / kScanWordsPerBlock;
   hipError_t e = hipSuccess;
-  if ((e = dalloc(&c->tab.slots, 16 * c->nlines)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->tab.slots, 8 * c->nlines)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.ent, 8 * c->max_flows)) != hipSuccess) return fail(map_err(e));
   // wide slots (non-IPv4-form keys): a power of two >= kSlotsPerFlow x max_flows,
   // at most 2^25 (2 GiB: K1's probe buffer resource and u32 offsets)
@@ -296,7 +296,10 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   while (c->tab.wide_mask + 1 < kSlotsPerFlow * c->max_flows && c->tab.wide_mask + 1 < (1ull << 25))
     c->tab.wide_mask = 2 * c->tab.wide_mask + 1;
   if ((e = dalloc(&c->tab.wide, 8 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
-  if ((e = hipMemset(c->tab.wide, 0, 64 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
+  // all ones, then every tag word zero (k_table_init sweeps the wide slots only once
+  // used): fs words ~0 as a reset leaves them
+  if ((e = hipMemset(c->tab.wide, 0xFF, 64 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
+  if ((e = hipMemset2D(c->tab.wide, 64, 0, 8, c->tab.wide_mask + 1)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.wide_used, 1)) != hipSuccess) return fail(map_err(e));
   if ((e = hipMemset(c->tab.wide_used, 0, 4)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.cnt, 2 * c->max_flows)) != hipSuccess) return fail(map_err(e));

@@ -17,26 +17,28 @@ constexpr uint32_t kStFlowFull = 1u, kStSpin = 2u, kStShard = 4u;
 // per-claim entries. A flow's claim index is its insertion order over the
 // context's life (fixed at insert; cmap[claim] = its dense first-seen id), so
 // claims are dense in [0, flows) and bounded by max_claims (= max_flows).
-//  slots: nlines lines of 128 B (u64[16]); open addressing, linear probing over
-//    slot s = line * 6 + pos:
-//    words 2*pos, 2*pos + 1 (pos < 6): w0, w1 of slot pos
+//  slots: nlines units of 64 B (u64[8]; half a 128-B cache line); open addressing,
+//    linear probing over slot s = unit * 3 + pos, for IPv4-form keys (12 zero bytes
+//    + the address, xdp.rs:116-119):
+//    words 2*pos, 2*pos + 1 (pos < 3): w0, w1 of slot pos
 //      w1 = kind << 56 | claim << 32 | lo32 (w1 == 0: empty; kind 1: busy)
-//      kind 2: an IPv4-form key (12 zero bytes + the address, xdp.rs:116-119):
-//              w0 = saddr | daddr << 32 (wire bytes), lo32 = sport | dport << 16 —
+//      kind 2: w0 = saddr | daddr << 32 (wire bytes), lo32 = sport | dport << 16 —
 //              the slot holds the whole key, so the slot alone decides a match
-//      kind 3: (not used: other keys live in the wide slots below)
-//      kind 4/5: dead (2/3 refused because the table was full): the key's w0 and
-//              lo32, no claim — the flow's later frames find it and stay unclassified
-//    bytes 96 + 4*pos: fs32 of slot pos: the batch-local first record index of a
+//      kind 4: dead (refused because the table was full): the key's w0 and lo32, no
+//              claim — the flow's later frames find it and stay unclassified
+//    bytes 48 + 4*pos: fs32 of slot pos: the batch-local first record index of a
 //      flow new in this batch (kFs32Flag | frame while only its claimer's mark is
-//      known); stale for flows of earlier batches (never read for them)
-//    One probe = one line (16-B slot + its fs32). kSlotsPerFlow slots per max_flow
-//    (load <= 1/8): ~171 B of slot lines per max_flow, 176 MB at 1M flows (rounds
-//    1-2: 64-B slots, 2-16 per max_flow, 512 MiB at bench's 1M flows). Measured
-//    (round 3, 125M IMIX frames, K1): load 1/2 costs 27 % at 10k flows and 29 % at
-//    1M (the linear-probe walks are dependent round trips); at equal load the
-//    compact lines match the 64-B slots (the cost of a large table is the probe's
-//    latency, not its bytes: a 44 MB table at load 1/2 was slower than 176 MB at 1/8).
+//      known); stale for flows of earlier batches (never read for them). A slot
+//      and its fs32 share the 64-B unit: the two 64-B halves of a line can be of
+//      different ages in L1/L2 (fs32 in the other half lost first_seen values)
+//    One probe = one 64-B unit (16-B slot + its fs32). kSlotsPerFlow slots per
+//    max_flow (load <= 1/8): ~171 B of slot units per max_flow, 176 MB at 1M flows
+//    (rounds 1-2: 64-B slots, 2-16 per max_flow, 512 MiB at bench's 1M flows).
+//    Measured (round 3, 125M IMIX frames, K1): load 1/2 costs 27 % at 10k flows and
+//    29 % at 1M (the linear-probe walks are dependent round trips); at equal load
+//    the compact slots match the 64-B slots (the cost of a large table is the
+//    probe's latency, not its bytes: a 44 MB table at load 1/2 was slower than
+//    176 MB at 1/8).
 //  ent [claim*8 + 0..4] the 40-B key as 5 LE u64 words; [claim*8 + 5] first_seen
 //      (global accepted-record index, written by K2); 6..7 spare
 //  cnt [id*2 + 0/1]    pkts / bytes of dense flow id `id`
@@ -59,7 +61,7 @@ struct FlowTable {
                          // [0, flows), so K3 stages it in LDS
   uint64_t max_claims;   // claims at or past it are refused (TCBEE_EFLOWFULL)
 };
-constexpr uint32_t kSlotsPerLine = 6;
+constexpr uint32_t kSlotsPerLine = 3;  // compact slots per 64-B unit
 constexpr uint32_t kWideSlot = 1u << 31;  // slot ids: compact s, or wide s | kWideSlot
 constexpr uint64_t kSlotsPerFlow = 8;  // slots per max_flow: linear-probe load <= 1/8
 constexpr uint32_t kFs32Flag = 1u << 31;

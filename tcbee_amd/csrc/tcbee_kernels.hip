@@ -315,14 +315,14 @@ __device__ __forceinline__ void st_agent32(uint32_t* p, uint32_t v) {
 }
 constexpr uint64_t kKindBusy = 1ull << 56;
 constexpr uint64_t kClaimBits = 0xFFFFFFull << 32;  // w1 bits 55:32
-__device__ __forceinline__ uint32_t slot_line(uint32_t s) { return __umulhi(s, 0xAAAAAAABu) >> 2; }  // s / 6
+__device__ __forceinline__ uint32_t slot_line(uint32_t s) { return __umulhi(s, 0xAAAAAAABu) >> 1; }  // s / 3
 __device__ __forceinline__ uint64_t* slot_ptr(const FlowTable& T, uint32_t s) {
   const uint32_t l = slot_line(s);
-  return T.slots + 16ull * l + 2u * (s - l * kSlotsPerLine);
+  return T.slots + 8ull * l + 2u * (s - l * kSlotsPerLine);
 }
 __device__ __forceinline__ uint32_t* slot_fs(const FlowTable& T, uint32_t s) {
   const uint32_t l = slot_line(s);
-  return reinterpret_cast<uint32_t*>(T.slots + 16ull * l + 12) + (s - l * kSlotsPerLine);
+  return reinterpret_cast<uint32_t*>(T.slots + 8ull * l + 6) + (s - l * kSlotsPerLine);
 }
 // home slot: line from the hash's high word (range reduction), position from its low bits
 __device__ __forceinline__ uint32_t home_slot(uint64_t h, uint64_t nlines) {
@@ -764,7 +764,7 @@ void k_parse(ParseArgs a) {
     // num_records = the slot lines' bytes (< 2^32: max_flows <= kMaxTableFlows; the
     // bits are read as unsigned), and the wide slots' (<= 2^31 bytes: see the ABI)
     const __amdgpu_buffer_rsrc_t sl_rs = __builtin_amdgcn_make_buffer_rsrc(
-        a.tab.slots, 0, (int)(uint32_t)(a.tab.nlines * 128u), 0x00020000);
+        a.tab.slots, 0, (int)(uint32_t)(a.tab.nlines * 64u), 0x00020000);
     const __amdgpu_buffer_rsrc_t wd_rs = __builtin_amdgcn_make_buffer_rsrc(
         a.tab.wide, 0, (int)(uint32_t)((a.tab.wide_mask + 1) * 64u), 0x00020000);
     bool uni[FPL], want[FPL];
@@ -790,8 +790,11 @@ void k_parse(ParseArgs a) {
         if (v4k[f]) {
           S0[f] = home_slot(h[f], a.tab.nlines);
           const uint32_t l = slot_line(S0[f]), pos = S0[f] - l * kSlotsPerLine;
-          Q[f][0] = __builtin_amdgcn_raw_buffer_load_b128(sl_rs, l * 128u + 16u * pos, 0, PROBE_AUX);
-          FS[f] = __builtin_amdgcn_raw_buffer_load_b32(sl_rs, l * 128u + 96u + 4u * pos, 0, PROBE_AUX);
+          Q[f][0] = __builtin_amdgcn_raw_buffer_load_b128(sl_rs, l * 64u + 16u * pos, 0, PROBE_AUX);
+          // (the slot and its fs32 share one 64-B half-line: the two halves of a
+          //  128-B line can be of different ages in L1/L2 — a fresh published slot
+          //  beside a stale fs32 lost first_seen values when fs32 sat in the other half)
+          FS[f] = __builtin_amdgcn_raw_buffer_load_b32(sl_rs, l * 64u + 48u + 4u * pos, 0, PROBE_AUX);
         } else {
           S0[f] = (uint32_t)(h[f] & a.tab.wide_mask);
 #pragma unroll
@@ -831,8 +834,8 @@ void k_parse(ParseArgs a) {
             if (step >= a.plain_walk) break;
             s = s + 1 == nslots ? 0u : s + 1;
             const uint32_t l = slot_line(s), pos = s - l * kSlotsPerLine;
-            const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(sl_rs, l * 128u + 16u * pos, 0, PROBE_AUX);
-            fsv = __builtin_amdgcn_raw_buffer_load_b32(sl_rs, l * 128u + 96u + 4u * pos, 0, PROBE_AUX);
+            const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(sl_rs, l * 64u + 16u * pos, 0, PROBE_AUX);
+            fsv = __builtin_amdgcn_raw_buffer_load_b32(sl_rs, l * 64u + 48u + 4u * pos, 0, PROBE_AUX);
             w0 = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
             w1 = (uint64_t)q[2] | ((uint64_t)q[3] << 32);
           }
@@ -981,14 +984,26 @@ void k_parse(ParseArgs a) {
 // ---------------------------------------------------------------------------
 // flow table init: tags/keys/ids 0, first_seen ~0, counters 0
 // ---------------------------------------------------------------------------
+// An empty slot unit: w0/w1 zero (empty); fs32 all ones, so a frame that reads a
+// snapshot of the unit older than its slot's claim mark competes for first_seen
+// (safe) instead of skipping (0 would lose the first record). Wide slots: tag word
+// 0 and fs word ~0, as rounds 1-2.
+__device__ __forceinline__ void empty_units(const FlowTable& t, uint64_t t0, uint64_t stride) {
+  uint4* L = reinterpret_cast<uint4*>(t.slots);
+  for (uint64_t q = t0; q < 4 * t.nlines; q += stride)
+    L[q] = (q & 3) == 3 ? make_uint4(~0u, ~0u, ~0u, 0u) : make_uint4(0u, 0u, 0u, 0u);
+  if (*t.wide_used)  // (cleared at context creation; swept only once used)
+    for (uint64_t w = t0; w <= t.wide_mask; w += stride) {
+      t.wide[8 * w] = 0;
+      t.wide[8 * w + 6] = ~0ull;
+    }
+}
+
 __global__ void k_table_init(FlowTable t) {
-  const uint64_t words = 16 * t.nlines;  // slot lines: every w1 (and fs32) zero = empty
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  for (uint64_t w = t0; w < words; w += stride) t.slots[w] = 0;
+  empty_units(t, t0, stride);
   for (uint64_t i = t0; i < 2 * t.max_claims; i += stride) t.cnt[i] = 0;
-  if (*t.wide_used)  // (zeroed at context creation; swept only once used)
-    for (uint64_t s = t0; s <= t.wide_mask; s += stride) t.wide[8 * s] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1007,11 +1022,8 @@ __global__ void k_prep(PrepArgs p) {
     // (claims restart at 0), and the by-id counters are zeroed by K2 as ids are
     // handed out (the previous batch's K3 may still be adding to them on another
     // stream)
-    uint4* L = reinterpret_cast<uint4*>(p.tab.slots);
-    for (uint64_t q = t0; q < 8 * p.tab.nlines; q += stride) L[q] = make_uint4(0u, 0u, 0u, 0u);
-    // wide slots: only their tag words, and only once a non-IPv4 key was claimed
-    if (*p.tab.wide_used)
-      for (uint64_t q = t0; q <= p.tab.wide_mask; q += stride) p.tab.wide[8 * q] = 0;
+    // (wide slots only once a non-IPv4 key was claimed)
+    empty_units(p.tab, t0, stride);
   }
 }
 
@@ -2833,7 +2845,7 @@ static unsigned grid_for(uint64_t n, unsigned cap = 4096) {
 }
 
 hipError_t launch_table_init(FlowTable t, hipStream_t s) {
-  hipLaunchKernelGGL(k_table_init, dim3(grid_for(8 * t.nlines)), dim3(kBlock), 0, s, t);
+  hipLaunchKernelGGL(k_table_init, dim3(grid_for(4 * t.nlines)), dim3(kBlock), 0, s, t);
   return hipGetLastError();
 }
 
@@ -2919,7 +2931,7 @@ hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s, 
 
 hipError_t launch_prep(const PrepArgs& p, hipStream_t s) {
   uint64_t work = p.ntiles;
-  if (p.reset && 8 * p.tab.nlines > work) work = 8 * p.tab.nlines;
+  if (p.reset && 4 * p.tab.nlines > work) work = 4 * p.tab.nlines;
   // (the wide-slot sweep, when it runs, is grid-strided over the same launch)
   hipLaunchKernelGGL(k_prep, dim3(grid_for(work < 4 ? 4 : work)), dim3(kBlock), 0, s, p);
   return hipGetLastError();
