@@ -46,6 +46,7 @@ struct tcbee_ctx {
   uint64_t* d_tile_status = nullptr;
   uint64_t max_tiles = 0;
   uint64_t* d_new_list = nullptr;
+  uint32_t* d_new_fs = nullptr;     // K2 scratch: new flows' local first_seen
   uint32_t* d_bitmap = nullptr;
   uint32_t* d_wprefix = nullptr;
   uint32_t* d_bprefix = nullptr;
@@ -187,6 +188,8 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   dfree(c->tab.slots);
   dfree(c->tab.ent);
+  dfree(c->tab.cfs);
+  dfree(c->d_new_fs);
   dfree(c->tab.wide);
   dfree(c->tab.wide_used);
   dfree(c->tab.cnt);
@@ -290,6 +293,8 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   hipError_t e = hipSuccess;
   if ((e = dalloc(&c->tab.slots, 8 * c->nlines)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.ent, 8 * c->max_flows)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->tab.cfs, c->max_flows)) != hipSuccess) return fail(map_err(e));
+  if ((e = dalloc(&c->d_new_fs, c->max_flows)) != hipSuccess) return fail(map_err(e));
   // wide slots (non-IPv4-form keys): a power of two >= kSlotsPerFlow x max_flows,
   // at most 2^25 (2 GiB: K1's probe buffer resource and u32 offsets)
   c->tab.wide_mask = 63;
@@ -497,6 +502,7 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
   if (flows && ntiles > 0) {
     RankArgs r{};
     r.new_list = c->d_new_list;
+    r.new_fs = c->d_new_fs;
     r.batch = c->d_batch;
     r.persist = c->d_persist;
     r.tab = c->tab;
@@ -540,7 +546,7 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     // A/B: TCBEE_K3ABL=93 the round-2 k_count_chunk (16384 records, 132 KiB, one
     // workgroup per CU); 92: its 8192-record form (512 threads, two per CU) — slower
     // in round 2 than 16384: 125k flows 5.60 vs 5.72 ms/step, 1M flows 7.51 vs 7.77
-    k.chunk = c->k3_variant == 92 ? 8192u : c->k3_variant == 93 ? 16384u : 12288u;
+    k.chunk = (c->k3_variant == 92 || c->k3_variant == 95) ? 8192u : c->k3_variant == 93 ? 16384u : 12288u;
     // trade-off: more blocks = more latency hidden; each block writes a partial row
     // of every flow, so a block should see a few thousand records; and a block
     // never covers more than kK3MaxPer records (bin fields cannot overflow)
@@ -806,10 +812,11 @@ int tcbee_flow_export(tcbee_ctx* c, tcbee_flow_entry* out, uint64_t cap, uint64_
   TRY_HIP(hipMemcpyAsync(&p, c->d_persist, sizeof(p), hipMemcpyDeviceToHost, c->stream));
   TRY_HIP(hipStreamSynchronize(c->stream));
   const uint64_t nf = p.flow_count;
-  std::vector<uint64_t> ent, cnt;
+  std::vector<uint64_t> ent, cnt, cfs;
   std::vector<uint32_t> cmap;
   try {
     ent.resize(8 * nf + 1);
+    cfs.resize(nf + 1);
     cnt.resize(2 * nf + 2);
     cmap.resize(nf + 1);
   } catch (...) {
@@ -819,6 +826,7 @@ int tcbee_flow_export(tcbee_ctx* c, tcbee_flow_entry* out, uint64_t cap, uint64_
     TRY_HIP(hipMemcpyAsync(ent.data(), c->tab.ent, 8 * nf * 8, hipMemcpyDeviceToHost, c->stream));
     TRY_HIP(hipMemcpyAsync(cnt.data(), c->tab.cnt, 2 * nf * 8, hipMemcpyDeviceToHost, c->stream));
     TRY_HIP(hipMemcpyAsync(cmap.data(), c->tab.cmap, nf * 4, hipMemcpyDeviceToHost, c->stream));
+    TRY_HIP(hipMemcpyAsync(cfs.data(), c->tab.cfs, nf * 8, hipMemcpyDeviceToHost, c->stream));
     TRY_HIP(hipStreamSynchronize(c->stream));
   }
   for (uint64_t cl = 0; cl < nf; ++cl) {  // claims; ids are a permutation of [0, nf)
@@ -829,7 +837,7 @@ int tcbee_flow_export(tcbee_ctx* c, tcbee_flow_entry* out, uint64_t cap, uint64_
     std::memcpy(e.tuple, m, TCBEE_KEY_BYTES);
     e.pkts = cnt[2 * id];
     e.bytes = cnt[2 * id + 1];
-    e.first_seen = m[5];
+    e.first_seen = cfs[cl];
   }
   *n = nf < cap ? nf : cap;
   return TCBEE_OK;
@@ -940,6 +948,7 @@ int tcbee_flow_merge_device(tcbee_ctx* c, const tcbee_flow_entry* ent_dev, uint6
   g.bitmap = c->d_mbitmap;
   RankArgs r{};
   r.new_list = c->d_new_list;
+  r.new_fs = c->d_new_fs;
   r.batch = c->d_batch;
   r.persist = c->d_persist;
   r.tab = c->tab;

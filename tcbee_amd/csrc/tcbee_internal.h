@@ -39,13 +39,14 @@ constexpr uint32_t kStFlowFull = 1u, kStSpin = 2u, kStShard = 4u;
 //    the compact slots match the 64-B slots (the cost of a large table is the
 //    probe's latency, not its bytes: a 44 MB table at load 1/2 was slower than
 //    176 MB at 1/8).
-//  ent [claim*8 + 0..4] the 40-B key as 5 LE u64 words; [claim*8 + 5] first_seen
-//      (global accepted-record index, written by K2); 6..7 spare
+//  ent [claim*8 + 0..4] the 40-B key as 5 LE u64 words (5..7 spare)
+//  cfs [claim]         first_seen (global accepted-record index, written by K2)
 //  cnt [id*2 + 0/1]    pkts / bytes of dense flow id `id`
 struct FlowTable {
   uint64_t* slots;
   uint64_t nlines;
   uint64_t* ent;
+  uint64_t* cfs;         // [claim] first_seen (global accepted-record index), by K2
   // wide slots (64 B, rounds 1-2's layout) for keys that are not IPv4-form: the
   // 40-B key lives in the slot, so an IPv6 probe is one line and compares at once
   // (a compact kind-3 slot + its entry cost K1 15 % on an all-IPv6 trace: a
@@ -133,6 +134,7 @@ struct RankArgs {
   uint32_t* bitmap;     // one bit per accepted frame of the batch
   uint32_t* wprefix;    // per bitmap word: exclusive popcount prefix in its block
   uint32_t* bprefix;    // per scan block: exclusive popcount prefix
+  uint32_t* new_fs;     // [max_claims] k_mark's copy of each new flow's local first_seen
   uint64_t nwords;
   uint64_t nblocks;
   bool update_persist;  // parse (not merge): advance rec_base / flow_count when

@@ -1085,7 +1085,7 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
         const uint4 q = v4[i];
         rank += (q.x < v) + (q.y < v) + (q.z < v) + (q.w < v);
       }
-      r.tab.ent[8 * (fbase + j) + 5] = base + v;  // first_seen, global record index
+      r.tab.cfs[fbase + j] = base + v;  // first_seen, global record index
       r.tab.cmap[fbase + j] = (uint32_t)(fbase + rank);
       if (r.update_persist) r.tab.cnt[2 * (fbase + rank)] = r.tab.cnt[2 * (fbase + rank) + 1] = 0;
     }
@@ -1160,7 +1160,7 @@ __global__ __launch_bounds__(1024) void k_rank_small(RankArgs r) {
                              ((1u << (local & 31)) - 1u);
       id = fbase + r.wprefix[w] + __popc(below);
     }
-    r.tab.ent[8 * (fbase + j) + 5] = base + local;
+    r.tab.cfs[fbase + j] = base + local;
     r.tab.cmap[fbase + j] = (uint32_t)id;
     if (r.update_persist) r.tab.cnt[2 * id] = r.tab.cnt[2 * id + 1] = 0;
   }
@@ -1174,6 +1174,7 @@ __global__ __launch_bounds__(kBlock) void k_mark(RankArgs r) {
   for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n_new;
        j += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t local = new_flow_fs(r, j);
+    r.new_fs[j] = (uint32_t)local;  // k_assign reads it densely (not through the slots)
     if ((local >> 5) < r.nwords) {
       atomicOr(&r.bitmap[local >> 5], 1u << (local & 31));
       wmax = (local >> 5) > wmax ? (local >> 5) : wmax;
@@ -1282,14 +1283,14 @@ __global__ void k_assign(RankArgs r) {
   const uint64_t fbase = r.persist->rank_fbase;
   for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n_new;
        j += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t local = new_flow_fs(r, j);
+    const uint64_t local = r.new_fs[j];  // (k_mark's copy of the slot's fs32)
     const uint64_t w = local >> 5;
     uint64_t id = fbase + n_new - 1;  // first_seen outside the batch: see k_rank_small
     if (w < lim) {
       const uint32_t below = r.bitmap[w] & ((1u << (local & 31)) - 1u);
       id = fbase + r.bprefix[w / kScanWordsPerBlock] + r.wprefix[w] + __popc(below);
     }
-    r.tab.ent[8 * (fbase + j) + 5] = base + local;
+    r.tab.cfs[fbase + j] = base + local;
     r.tab.cmap[fbase + j] = (uint32_t)id;
     if (r.update_persist) r.tab.cnt[2 * id] = r.tab.cnt[2 * id + 1] = 0;
   }
@@ -1973,9 +1974,9 @@ __global__ __launch_bounds__(BS) void k_count_chunk(CountArgs c) {
 // the region entry at region[chunk + idx] and the id back into s_rw[pos] — a slot
 // only its own reader touches, so no barrier between the gather and the write-back.
 constexpr uint32_t kLenSat = 2047;  // caplens >= kLenSat are re-read from the K1 scratch
-template <bool PACK, int BS, int U>
-// (two workgroups of BS / 64 waves on a CU's 4 SIMDs: BS / 128 waves per SIMD)
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(BS / 128, 8)))
+template <bool PACK, int BS, int U, int WG_PER_CU = 2>
+// (WG_PER_CU workgroups of BS / 64 waves on a CU's 4 SIMDs)
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WG_PER_CU * BS / 256, 8)))
 void k_count_chunk2(CountArgs c) {
   constexpr int CH = U * BS;
   __shared__ uint32_t s_rw[CH];
@@ -2009,25 +2010,35 @@ void k_count_chunk2(CountArgs c) {
       w[k] = __builtin_nontemporal_load(&af[pos < nval ? pos : 0u]);
       if (!PACK) lp[k] = __builtin_nontemporal_load(&al[pos < nval ? pos : 0u]);  // (lp: len)
     }
+    // decode: claim | min(caplen, kLenSat) << 21 (~0: no flow). A caplen of
+    // >= kLenSat (2047 B: never on an IMIX trace) is rare: the wave then redoes its
+    // words with the full value (the side array when the packed field saturated) and
+    // sends a caplen past the region field to the flow's counter by a device atomic;
+    // the common path has no per-word branches (their exec masks cost registers)
+    bool rare = false;
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const uint32_t pos = (uint32_t)k * BS + tid;
       const uint32_t v = w[k];
-      uint32_t cl, len;
-      if (PACK) {
-        cl = v == 0xFFFFFFFFu ? v : (v & ((1u << c.pack_bits) - 1u));
-        len = v >> c.pack_bits;
-        if (len == lmax && cl != 0xFFFFFFFFu) len = al[pos];  // saturated: the side array
-      } else {
-        cl = v;
-        len = lp[k];
-      }
+      uint32_t cl = PACK ? (v == 0xFFFFFFFFu ? v : (v & ((1u << c.pack_bits) - 1u))) : v;
+      const uint32_t len = PACK ? (v >> c.pack_bits) : lp[k];
       if (pos >= nval) cl = 0xFFFFFFFFu;
-      const bool big = len >= kRegLenEsc;
-      if (big && cl != 0xFFFFFFFFu)
-        atomicAdd((unsigned long long*)&c.cnt[2ull * c.cmap[cl] + 1], (unsigned long long)len);
-      const uint32_t l = big ? 0u : (len < kLenSat ? len : kLenSat);
-      w[k] = cl == 0xFFFFFFFFu ? 0xFFFFFFFFu : (cl | l << 21);
+      rare |= cl != 0xFFFFFFFFu && len >= kLenSat;
+      w[k] = cl == 0xFFFFFFFFu ? 0xFFFFFFFFu : (cl | (len < kLenSat ? len : kLenSat) << 21);
+    }
+    if (__any(rare)) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint32_t pos = (uint32_t)k * BS + tid;
+        const uint32_t cl = w[k] == 0xFFFFFFFFu ? w[k] : (w[k] & 0x1FFFFFu);
+        if (cl == 0xFFFFFFFFu || (w[k] >> 21) != kLenSat) continue;
+        uint32_t len = PACK ? (af[pos] >> c.pack_bits) : al[pos];
+        if (PACK && len == lmax) len = al[pos];  // saturated packed field: the side array
+        if (len >= kRegLenEsc) {  // past the region entry's field: counted here
+          atomicAdd((unsigned long long*)&c.cnt[2ull * c.cmap[cl] + 1], (unsigned long long)len);
+          w[k] = cl;  // caplen 0 in the region entry
+        }
+      }
     }
 #pragma unroll
     for (int k = 0; k < U; ++k) {
@@ -2131,7 +2142,32 @@ __global__ __launch_bounds__(kCountBlock) void k_count_bucket(CountArgs c, uint3
   // Every region load is independent of the others, so short runs (1M flows: 245
   // buckets, ~50 records per chunk and bucket) no longer cost a dependent offset ->
   // data round trip each (round 2: 0.43 ms per 125M records at 1M flows).
-  const uint64_t K = G > s ? (G - s + S - 1) / S : 0;
+  // Runs of >= 256 records on average (few buckets: 125k flows = 31 buckets,
+  // ~400 records per chunk and bucket) go one segment per wave, 4 loads per lane in
+  // flight: the run hides the offset round trip, and the flattened walk's scalar
+  // segment tracking cost more there (125M records: 166 vs 210 us)
+  if (per / nb >= 256) {
+    for (uint64_t q = s + S * wave; q < G; q += S * kWaves) {
+      const uint64_t lo_q = q * per;
+      if (lo_q >= n_acc) break;
+      const uint32_t* o = obase + q * ostride;
+      const uint64_t a0 = lo_q + o[j], a1 = lo_q + o[j + 1];
+      for (uint64_t x = a0 + lane; x < a1; x += 256) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          v[u] = __builtin_nontemporal_load(&c.region[x + 64u * u < a1 ? x + 64u * u : x]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (x + 64u * u >= a1) continue;
+          const uint32_t t = v[u] & (kBucket - 1);
+          atomicAdd((unsigned long long*)&s_pk[t], 1ull);
+          atomicAdd((unsigned long long*)&s_by[t], (unsigned long long)(v[u] >> kBucketBits));
+        }
+      }
+    }
+  }
+  const uint64_t K = per / nb >= 256 ? 0 : (G > s ? (G - s + S - 1) / S : 0);
   for (uint64_t kb = (uint64_t)wave * 64; kb < K; kb += 64ull * kWaves) {
     const uint64_t k = kb + lane;
     uint64_t st = 0;
@@ -2330,7 +2366,7 @@ __global__ void k_export(FlowTable t, uint64_t* out, uint64_t cap, const Persist
   const uint64_t nflows = p->flow_count;
   for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nflows;
        c += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t* m = t.ent + 8 * c;  // key m[0..4], first_seen m[5]
+    const uint64_t* m = t.ent + 8 * c;  // key m[0..4]
     const uint64_t id = t.cmap[c];
     if (id >= cap) continue;
     uint64_t* e = out + 8 * id;
@@ -2338,7 +2374,7 @@ __global__ void k_export(FlowTable t, uint64_t* out, uint64_t cap, const Persist
     for (int j = 0; j < 5; ++j) e[j] = m[j];
     e[5] = t.cnt[2 * id];
     e[6] = t.cnt[2 * id + 1];
-    e[7] = m[5];
+    e[7] = t.cfs[c];
   }
   if (n_out && blockIdx.x == 0 && threadIdx.x == 0) {
     n_out[0] = nflows < cap ? nflows : cap;
@@ -2378,7 +2414,7 @@ __global__ void k_export_global(GlobalExportArgs g) {
     for (int j = 0; j < 5; ++j) e[j] = m[j];
     e[5] = g.tab.cnt[2 * id];
     e[6] = g.tab.cnt[2 * id + 1];
-    const uint64_t gfs = place_first(g, m[5], lo, hi, bad_batch);
+    const uint64_t gfs = place_first(g, g.tab.cfs[c], lo, hi, bad_batch);
     bad = bad || gfs == ~0ull;
     e[7] = gfs;
   }
@@ -2401,7 +2437,7 @@ __global__ void k_records_before(FlowTable t, const PersistState* p, const uint3
        c += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t id = t.cmap[c];
     if (id >= cap) continue;
-    const uint64_t G = t.ent[8 * c + 5];
+    const uint64_t G = t.cfs[c];
     uint64_t lo = 0, len = n;  // first record whose global frame >= G
     while (len > 0) {
       const uint64_t half = len >> 1, mid = lo + half;
@@ -2423,7 +2459,7 @@ __global__ void k_set_first_seen(FlowTable t, const PersistState* p, const uint6
   for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nflows;
        c += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t id = t.cmap[c];
-    if (id < cap) t.ent[8 * c + 5] = fs_by_id[id];
+    if (id < cap) t.cfs[c] = fs_by_id[id];
   }
 }
 
@@ -2446,7 +2482,7 @@ __global__ void k_first_frames(GlobalExportArgs g) {
        c += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t id = g.tab.cmap[c];
     if (id < fbase || id - fbase >= g.cap) continue;
-    const uint64_t gfs = place_first(g, g.tab.ent[8 * c + 5], lo, hi, bad_batch);
+    const uint64_t gfs = place_first(g, g.tab.cfs[c], lo, hi, bad_batch);
     bad = bad || gfs == ~0ull;
     g.out[id - fbase] = gfs;
   }
@@ -2554,7 +2590,7 @@ __global__ __launch_bounds__(kBlock) void k_owner_bucket(OwnerArgs a) {
     for (int j = 0; j < 5; ++j) out[j] = m[j];
     out[5] = 0;  // pkts / bytes: K3 has not run (the ids come first)
     out[6] = 0;
-    out[7] = m[5];  // first_seen, local to this rank's record stream
+    out[7] = a.tab.cfs[c];  // first_seen, local to this rank's record stream
     a.lid[e] = a.tab.cmap[c];
   }
   // meta[world + 1]: entries this rank dropped. Every rank sees it after the meta
@@ -2581,7 +2617,7 @@ __global__ void k_first_seen(FlowTable t, const PersistState* p, uint64_t* out, 
   for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nflows;
        c += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t id = t.cmap[c];
-    if (id < cap) out[id] = t.ent[8 * c + 5];
+    if (id < cap) out[id] = t.cfs[c];
   }
   if (n_out && blockIdx.x == 0 && threadIdx.x == 0) {
     n_out[0] = p->flow_count < cap ? p->flow_count : cap;
@@ -2993,7 +3029,11 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
     else hipLaunchKernelGGL((k_count_scatter_staged<4, false>), gs, dim3(kCountBlock), 0, s, c);
   }
   if (g2) {
-    if (c.coffs && c.chunk == 12u * 1024u) {  // 76 KiB of LDS: two workgroups per CU
+    if (c.coffs && c.chunk == 8u * 1024u && k3v == 95) {  // 52 KiB: three workgroups per CU (A/B)
+      const dim3 gc(g1s ? (g1s * 3 + 1) / 2 : 1);
+      if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk2<true, 512, 16, 3>), gc, dim3(512), 0, s, c);
+      else hipLaunchKernelGGL((k_count_chunk2<false, 512, 16, 3>), gc, dim3(512), 0, s, c);
+    } else if (c.coffs && c.chunk == 12u * 1024u) {  // 76 KiB of LDS: two workgroups per CU
       const dim3 gc(g1s ? g1s : 1);
       // 512-thread workgroups, 24 records per thread (TCBEE_K3ABL=94: 1024 x 12, A/B):
       // 125M records, 125k flows (packed words): 470 vs 476 us; 1M flows (unpacked):

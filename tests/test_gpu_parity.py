@@ -378,6 +378,40 @@ def test_flow_table_full_reports(gpu):
         assert p.status() == tcbee_amd._lib.EFLOWFULL
 
 
+@pytest.mark.parametrize("short", [0, 7])
+def test_flow_table_exact_capacity(gpu, oracle, short):
+    """max_flows bounds the claims exactly (round 3's compact table): a mixed trace
+    (IPv4-form keys in the 16-B compact slots, IPv6 keys in the 64-B wide slots)
+    with max_flows = its distinct flows is bit-exact with status OK; `short` flows
+    fewer refuse exactly that many flows (dead slots: their frames stay
+    unclassified, id ~0), records unchanged, TCBEE_EFLOWFULL; a second batch with
+    the table full finds the dead slots again (no new claims, no duplicates)."""
+    from tracegen import mixed_trace
+    tr = mixed_trace(60_000, seed=77, n_flows=2500)
+    rec, fh, fi, ctr, table = oracle.parse(tr)
+    cap = len(table) - short
+    with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 25, max_flows=cap) as p:
+        r1 = p.parse(tr.slice(0, 40_000))
+        r2 = p.parse(tr.slice(40_000, tr.n))
+        assert np.array_equal(np.concatenate([r1.records, r2.records]), rec)
+        ids = np.concatenate([r1.flow_id, r2.flow_id])
+        fl = p.flows()
+        if short == 0:
+            assert p.status() == 0
+            assert np.array_equal(ids, fi) and np.array_equal(fl, table)
+        else:
+            assert p.status() == tcbee_amd._lib.EFLOWFULL
+            assert len(fl) == cap
+            refused = ids == 0xFFFFFFFF
+            assert 0 < refused.sum() < len(ids)
+            # every record of a claimed flow carries an id < cap, and a flow's
+            # records are all claimed or all refused
+            assert ids[~refused].max() < cap
+            keys = np.unique(fi[refused])
+            assert not np.isin(fi[~refused], keys).any()
+            assert len(keys) == short
+
+
 def test_batch_over_1M_frames_multibatch(gpu, oracle):
     """Batches above 1M frames take the 4-kernel rank scan (bounded by the highest
     first-seen word, bitmap cleared again by K3); three batches, the second one
