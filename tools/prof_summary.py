@@ -162,6 +162,19 @@ def main():
             lines.append(f"| {v['workload']} | {v['read_B_per_frame']} | {v['write_B_per_frame']} | "
                          f"{v['traffic_B_per_frame']} | {v['rdreq_per_frame']} |")
         lines.append("")
+    c4f = os.path.join(OUT, "c4fprof", "run_kernel_stats.csv")
+    if os.path.exists(c4f):
+        shutil.copy(c4f, os.path.join(PROF, f"{tag}_config4_whole_kernel_stats.csv"))
+        lines += ["## config 4, the whole 1M-flow trace on one GPU", "",
+                  "Command: `rocprofv3 --kernel-trace --stats -- python bench.py --config4 "
+                  "--shard contig --steps 5 --warmup 1 --no-cpu --no-extra --sample-check` "
+                  "(125M IMIX frames, 1M flows: every flow in one table).", "",
+                  "| kernel | calls | avg us | total % |", "|---|---|---|---|"]
+        for r in csv.DictReader(open(c4f)):
+            if "tcbee" in r["Name"]:
+                lines.append(f"| `{r['Name'][:70]}` | {r['Calls']} | "
+                             f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} |")
+        lines.append("")
     small = os.path.join(OUT, "smallprof", "run_kernel_stats.csv")
     if os.path.exists(small):
         shutil.copy(small, os.path.join(PROF, f"{tag}_config2_kernel_stats.csv"))
