@@ -899,6 +899,8 @@ void k_parse(ParseArgs a) {
       if (acc[f]) asm volatile("" ::"v"(R[f][0]), "v"(R[f][5]), "v"(R[f][13]), "v"(R[f][17]));
   }
 
+  // (wave 0 resolving the look-back before its own probes instead — its inclusive
+  //  prefix published a probe phase earlier — was 22 % slower, round 3)
   if (wave == 0) {
     const uint64_t excl =
         (ABL & 1) ? tile * (uint64_t)TILE : lookback_resolve<TILE>(a, tile, total, withhold);
