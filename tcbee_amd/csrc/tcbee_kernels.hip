@@ -2149,24 +2149,39 @@ __global__ __launch_bounds__(kCountBlock) void k_count_bucket(CountArgs c, uint3
   // flight: the run hides the offset round trip, and the flattened walk's scalar
   // segment tracking cost more there (125M records: 166 vs 210 us)
   if (per / nb >= 256) {
+    // the next segment's offsets are loaded while this one is counted (one round
+    // trip less per segment), 8 records per lane in flight
+    auto offs_of = [&](uint64_t q, uint32_t& o0, uint32_t& o1) {
+      o0 = o1 = 0;
+      if (q < G && q * per < n_acc) {
+        const uint32_t* o = obase + q * ostride;
+        o0 = o[j];
+        o1 = o[j + 1];
+      }
+    };
+    uint32_t o0, o1;
+    offs_of(s + S * wave, o0, o1);
     for (uint64_t q = s + S * wave; q < G; q += S * kWaves) {
       const uint64_t lo_q = q * per;
       if (lo_q >= n_acc) break;
-      const uint32_t* o = obase + q * ostride;
-      const uint64_t a0 = lo_q + o[j], a1 = lo_q + o[j + 1];
-      for (uint64_t x = a0 + lane; x < a1; x += 256) {
-        uint32_t v[4];
+      uint32_t n0, n1;
+      offs_of(q + S * kWaves, n0, n1);
+      const uint64_t a0 = lo_q + o0, a1 = lo_q + o1;
+      for (uint64_t x = a0 + lane; x < a1; x += 512) {
+        uint32_t v[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 8; ++u)
           v[u] = __builtin_nontemporal_load(&c.region[x + 64u * u < a1 ? x + 64u * u : x]);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {
           if (x + 64u * u >= a1) continue;
           const uint32_t t = v[u] & (kBucket - 1);
           atomicAdd((unsigned long long*)&s_pk[t], 1ull);
           atomicAdd((unsigned long long*)&s_by[t], (unsigned long long)(v[u] >> kBucketBits));
         }
       }
+      o0 = n0;
+      o1 = n1;
     }
   }
   const uint64_t K = per / nb >= 256 ? 0 : (G > s ? (G - s + S - 1) / S : 0);

@@ -149,5 +149,6 @@ def test_exchange_calls_validate_before_device_work():
     assert L.tcbee_owner_apply_device(q, q, p, 2, 4, None, 8, None) == E
     # context calls with no context
     assert L.tcbee_owner_bucket_device(None, 2, 4, 8, p, q, p, None) == E
+    assert L.tcbee_status_raise_device(None, p, 2, 4, None) == E
     assert L.tcbee_flow_first_seen_device(None, p, 4, p, None) == E
     assert L.tcbee_flow_first_frames_device(None, p, 4, p, None, p, 4, 4, None) == E
