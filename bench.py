@@ -161,7 +161,9 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     # 1/8), 6 slots per 128-B line: 176 MB at 1M flows (rounds 1-2: 64-B slots at
     # max_flows = 4x flows, 512 MiB), and a tight max_flows keeps the K1 -> K3 word
     # packed (claim | caplen) up to 2^20 flows
-    cap = max(flows_here + flows_here // 32 + 64, 64)
+    # (+4 sigma of a binomial shard size on top, so no seed's RSS spread can refuse
+    # a flow; 1M flows stay below 2^20 + ... = packed K1 -> K3 words)
+    cap = max(flows_here + int(4 * flows_here ** 0.5) + flows_here // 32 + 64, 64)
     # (the exchange carries up to xcap entries per rank: a quarter more than the
     # shard's expected flows)
     xcap = max(int(1.25 * flows_here) + 4096, 1 << 12)
