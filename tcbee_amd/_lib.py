@@ -12,6 +12,10 @@ import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libtcbee_amd.so")
+# A/B tooling only (tools/lib_ab.sh: the same workload against an older build of the
+# kernels in another process); the product and the tests load the in-tree library
+if os.environ.get("TCBEE_AB_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["TCBEE_AB_LIB"])
 
 RECORD_BYTES = 74
 TRACE_BYTES = 72
