@@ -667,7 +667,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // ---------------------------------------------------------------------------
 // ABL: timing-only ablation bits (0 in every product launch; see tools/ablate.py)
 //   1 no look-back, 2 no record stores, 4 no header loads, 8 no index loads,
-//   16 no side outputs
+//   16 no side outputs, 32 no first-seen competition (atomicMin)
 // STAGE 0: the whole tile's records staged in LDS, stored by the block after the
 // look-back; STAGE 1: each wave stages and stores its own 64-record group per
 // round (its records are contiguous in the output), 4.7 KB of LDS per wave.
@@ -940,6 +940,7 @@ void k_parse(ParseArgs a) {
   // ---- per-record side outputs; first_seen = min accepted index ----
   // (pkts/bytes are NOT counted here: per-record memory-side atomics cost more
   //  than the whole parse; k_count histograms them by dense id in LDS.)
+  uint32_t prev_s0 = 0xFFFFFFFFu;  // slot of the wave's last all-one-slot new-flow group
 #pragma unroll
   for (int f = 0; f < FPL; ++f) {
     const uint64_t p = excl + rank[f];
@@ -962,7 +963,7 @@ void k_parse(ParseArgs a) {
         }
       }
     }
-    if (FLOWS) {
+    if (FLOWS && !(ABL & 32)) {
       // first_seen competition: only flows new in this batch (claim >= fbase)
       const bool mine = acc[f] && slot[f] != 0xFFFFFFFFu && claim[f] >= fbase;
       const uint64_t am = __ballot(mine);
@@ -972,8 +973,12 @@ void k_parse(ParseArgs a) {
         const uint32_t p32 = (uint32_t)p;
         const uint32_t frame_i = (uint32_t)(i0 + (uint64_t)f * BLK + tid);
         if (__all(!mine || slot[f] == s0)) {
-          // leader = lowest rank of the wave = its smallest accepted index
-          if (lane == leader && fs_needs_min(fs_seen[f], frame_i, p32))
+          // leader = lowest rank of the wave = its smallest accepted index; when the
+          // wave's previous frame group was all this slot too, its earlier leader
+          // competes for both (a hot new flow: one add per wave, not per group)
+          const bool first = s0 != prev_s0;
+          prev_s0 = s0;
+          if (first && lane == leader && fs_needs_min(fs_seen[f], frame_i, p32))
             atomicMin(slot_fs_any(a.tab, s0), p32);
         } else if (mine && fs_needs_min(fs_seen[f], frame_i, p32)) {
           atomicMin(slot_fs_any(a.tab, slot[f]), p32);
@@ -2941,7 +2946,7 @@ static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s
     return hipGetLastError();
     switch (abl) {
       TCBEE_ABL_CASE(1) TCBEE_ABL_CASE(2) TCBEE_ABL_CASE(4) TCBEE_ABL_CASE(8)
-      TCBEE_ABL_CASE(16) TCBEE_ABL_CASE(3) TCBEE_ABL_CASE(31)
+      TCBEE_ABL_CASE(16) TCBEE_ABL_CASE(3) TCBEE_ABL_CASE(31) TCBEE_ABL_CASE(32)
       default: break;
     }
 #undef TCBEE_ABL_CASE

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--var", default="", help="extra env A/B, e.g. TCBEE_K3ABL=0,2")
     ap.add_argument("--flows-only", action="store_true", help="only the flows-on variants")
     ap.add_argument("--cap-mult", default="4", help="max_flows = mult x flows (comma list: A/B)")
+    ap.add_argument("--warm", action="store_true", help="keep the flow table across steps (no reset)")
     args = ap.parse_args()
     import torch
     import tcbee_amd
@@ -71,7 +72,8 @@ def main():
             for v in variants:
                 p = parsers[v]
                 def step():
-                    p.reset_flows(stream=stream, sync=False)  # one fresh trace per step, as bench.py
+                    if not args.warm:
+                        p.reset_flows(stream=stream, sync=False)  # one fresh trace per step, as bench.py
                     p.parse_device(d_arena, alen, d_off, d_len, d_ts, n, d_rec, n,
                                    d_hash if v[1] else None, d_id if v[1] else None, d_n, d_ctr,
                                    flows=v[1], stream=stream)

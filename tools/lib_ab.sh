@@ -9,17 +9,20 @@ cd "$(dirname "$0")/.."
 case "${1:-}" in
   build)
     rev=${2:-HEAD}
-    d=build/ab_$rev
+    d=build/ab_${rev//:/_}
     rm -rf "$d"; mkdir -p "$d/tcbee_amd/csrc" "$d/include"
+    # REV "wt:NAME": the working tree as it is now, kept under build/ab_wt:NAME
     for f in tcbee_kernels.hip tcbee_capi.hip tcbee_pipe.hip tcbee_gen.h tcbee_internal.h tcbee_layout.h; do
-      git show "$rev:tcbee_amd/csrc/$f" > "$d/tcbee_amd/csrc/$f"
+      case $rev in wt:*) cp "tcbee_amd/csrc/$f" "$d/tcbee_amd/csrc/$f" ;;
+                   *) git show "$rev:tcbee_amd/csrc/$f" > "$d/tcbee_amd/csrc/$f" ;; esac
     done
-    git show "$rev:include/tcbee_amd.h" > "$d/include/tcbee_amd.h"
+    case $rev in wt:*) cp include/tcbee_amd.h "$d/include/tcbee_amd.h" ;;
+                 *) git show "$rev:include/tcbee_amd.h" > "$d/include/tcbee_amd.h" ;; esac
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -shared \
       -o "$d/libtcbee_amd.so" "$d/tcbee_amd/csrc/tcbee_kernels.hip" "$d/tcbee_amd/csrc/tcbee_capi.hip" "$d/tcbee_amd/csrc/tcbee_pipe.hip"
     echo "$d/libtcbee_amd.so" ;;
   run)
     rev=$2; shift 3
-    TCBEE_AB_LIB=build/ab_$rev/libtcbee_amd.so "$@" ;;
+    TCBEE_AB_LIB=build/ab_${rev//:/_}/libtcbee_amd.so "$@" ;;
   *) echo "usage: $0 build [REV] | run REV -- CMD..." >&2; exit 2 ;;
 esac
