@@ -62,11 +62,39 @@ def build_device_trace(torch, n, sizes, kind, n_flows, seed, first_index, stream
     return d_arena, alen, d_off, d_len, d_ts
 
 
-def build_shard_trace(torch, n_global, world, rank, sizes, kind, n_flows, seed, stream):
+RSS_WINDOW = 16_000_000  # frames of observed traffic an RSS table is balanced on
+
+
+def rss_for(torch, n_global, world, kind, n_flows, seed, stream):
+    """The NIC's RSS indirection table (4096 hash buckets -> GPUs) balanced on the
+    bucket loads of the trace's first RSS_WINDOW frames (tcbee_gen_rss_load_device,
+    tcbee_amd.rss_table; the same table on every rank), as receive-side scaling is
+    rebalanced from observed load. Every flow still lands on one GPU. Returns the
+    table on the device and what the line reports (TCBEE_BENCH_RSS=0: None, the
+    modulo placement fold32(hash) % world)."""
+    import tcbee_amd
+    if world < 2 or os.environ.get("TCBEE_BENCH_RSS", "1") == "0":
+        return None, {"rss": None}
+    win = min(n_global, RSS_WINDOW)
+    counts = torch.empty(tcbee_amd.RSS_BUCKETS, dtype=torch.int64, device="cuda")
+    tcbee_amd.gen_rss_load_device(win, kind, n_flows, seed, counts, stream=stream)
+    load = counts.cpu().numpy()
+    table = tcbee_amd.rss_table(load, world)
+    per = np.bincount(table, weights=load, minlength=world)
+    info = {"rss": {"buckets": len(table), "balanced_on_frames": win,
+                    "window_imbalance": round(float(per.max() / per.mean()), 5)}}
+    if len(table) % world == 0:  # the modulo placement on the same window, for reference
+        mod = np.bincount(np.arange(len(table)) % world, weights=load, minlength=world)
+        info["rss"]["window_imbalance_modulo"] = round(float(mod.max() / mod.mean()), 5)
+    return torch.from_numpy(table.view(np.int16)).cuda(), info
+
+
+def build_shard_trace(torch, n_global, world, rank, sizes, kind, n_flows, seed, stream,
+                      rss=None):
     """This rank's flow-hash shard of the global synthetic trace [0, n_global) (the
     NIC-RSS view of config 4), built on the device: global indices + caplens
-    (tcbee_gen_shard_index_device), offsets by a prefix sum, headers by the device
-    generator at each frame's global index."""
+    (tcbee_gen_shard_index_device; with an RSS table, _rss_device), offsets by a
+    prefix sum, headers by the device generator at each frame's global index."""
     import tcbee_amd
     scratch = torch.empty(tcbee_amd.gen_shard_scratch_words(n_global), dtype=torch.int64,
                           device="cuda")
@@ -77,13 +105,13 @@ def build_shard_trace(torch, n_global, world, rank, sizes, kind, n_flows, seed, 
     # the sampling noise of the frame draw
     tcbee_amd.gen_shard_index_device(n_global, world, rank, kind, n_flows, seed,
                                      sizes == "imix", None, None, 0, scratch, n_out,
-                                     stream=stream)
+                                     stream=stream, rss=rss)
     cap = int(n_out.item())
     gidx = torch.empty(max(cap, 1), dtype=torch.int64, device="cuda")
     clen = torch.empty(max(cap, 1), dtype=torch.int32, device="cuda")
     tcbee_amd.gen_shard_index_device(n_global, world, rank, kind, n_flows, seed,
                                      sizes == "imix", gidx, clen, cap, scratch, n_out,
-                                     stream=stream)
+                                     stream=stream, rss=rss)
     m = int(n_out.item())
     if m != cap:
         raise RuntimeError(f"shard of {m} frames, counted {cap}")
@@ -119,8 +147,9 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     if flowhash:
         # n frames per GPU on average: rank `rank` parses the frames of ITS flows out of
         # a global trace of n * world frames (sizes differ by a few hundred)
+        rss, rss_info = rss_for(torch, n_global, sw, kind, n_flows, seed, stream)
         d_arena, alen, d_off, d_len, d_ts, gidx, n = build_shard_trace(
-            torch, n_global, sw, rank, sizes, kind, n_flows, seed, stream)
+            torch, n_global, sw, rank, sizes, kind, n_flows, seed, stream, rss=rss)
         first = 0
     else:
         d_arena, alen, d_off, d_len, d_ts = build_device_trace(torch, n, sizes, kind, n_flows,
@@ -292,6 +321,7 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
             check["exchange_entries_per_rank"] = xcap
     if flowhash:
         check["frames_local"] = n
+        check.update(rss_info)
         # every rank checks its own shard (global ids included) against the oracle
         check.update(validate_shard(torch, last["rec"], last["hash"], last["id"], gidx, n,
                                     sizes, kind, n_flows, seed, nrec, global_ids=multi))

@@ -38,7 +38,8 @@
 extern "C" {
 #endif
 
-#define TCBEE_ABI_VERSION 3  /* 3: owner meta world+2 words, tcbee_status_raise_device */
+#define TCBEE_ABI_VERSION 4  /* 3: owner meta world+2 words, tcbee_status_raise_device;
+                                4: RSS indirection tables for the shard generator */
 
 /* ---- record / key layout constants (DESIGN.md "Data layout") ------------ */
 #define TCBEE_RECORD_BYTES   74  /* tcp_packet.rs:42 ENTRY_SIZE            */
@@ -404,6 +405,21 @@ int tcbee_gen_shard_index_device(uint64_t n_global, int world, int rank, int kin
                                  uint64_t n_flows, uint64_t seed, int imix,
                                  uint64_t* out_gidx_dev, uint32_t* out_caplen_dev, uint64_t cap,
                                  uint64_t* scratch_dev, uint64_t* n_out_dev, void* stream);
+/* ABI 4. The same with a NIC's RSS indirection table: frame i goes to GPU
+ * rss_dev[fold32(flow_hash64(key)) % rss_len] (entries < world; rss_len <= 4096;
+ * rss_dev NULL = the modulo above), so a table can balance the GPUs' loads while
+ * every flow still lands on exactly one GPU. */
+int tcbee_gen_shard_index_rss_device(uint64_t n_global, int world, int rank, int kind,
+                                     uint64_t n_flows, uint64_t seed, int imix,
+                                     const uint16_t* rss_dev, uint32_t rss_len,
+                                     uint64_t* out_gidx_dev, uint32_t* out_caplen_dev,
+                                     uint64_t cap, uint64_t* scratch_dev, uint64_t* n_out_dev,
+                                     void* stream);
+/* ABI 4. Frames per RSS bucket (fold32(flow_hash64(key)) % rss_len) over global
+ * frames [0, n_frames) of the synthetic trace: counts_dev[rss_len] u64 (overwritten),
+ * the observed load a table is balanced on (tcbee_amd.trace.rss_table). Asynchronous. */
+int tcbee_gen_rss_load_device(uint64_t n_frames, int kind, uint64_t n_flows, uint64_t seed,
+                              uint32_t rss_len, uint64_t* counts_dev, void* stream);
 
 /* ---- ingest pipeline: host frames -> records on the host ----------------
  * (replaces the live ring drain of

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define TCBEE_HOST_ABI_VERSION 1
+#define TCBEE_HOST_ABI_VERSION 2  /* 2: RSS indirection tables (tcbee_flowhash_owner_rss, _load) */
 int tcbee_host_abi_version(void);
 
 /* ---- classic pcap ---------------------------------------------------------
@@ -69,6 +69,18 @@ int tcbee_pcap_write(const char* path, const tcbee_frames* in, int nanosecond,
  * owning GPU's hook. threads 0 = 1. */
 int tcbee_flowhash_owner(const tcbee_frames* in_host, uint32_t world, uint32_t threads,
                          uint16_t* out_owner);
+/* Host ABI 2. The NIC's RSS indirection table: a keyed frame goes to GPU
+ * rss[fold32(flow_hash64(key)) % rss_len] (every entry < world, rss_len <=
+ * TCBEE_RSS_MAX; rss NULL = the modulo above), the same placement as
+ * tcbee_gen_shard_index_rss_device. A table balanced on observed bucket loads
+ * (tcbee_flowhash_load, tcbee_amd.trace.rss_table) evens out the GPUs' frame
+ * counts while every flow still reaches exactly one GPU. */
+#define TCBEE_RSS_MAX 4096
+int tcbee_flowhash_owner_rss(const tcbee_frames* in_host, uint32_t world, const uint16_t* rss,
+                             uint32_t rss_len, uint32_t threads, uint16_t* out_owner);
+/* Keyed frames per RSS bucket (fold32(flow_hash64(key)) % rss_len): out_counts[rss_len]. */
+int tcbee_flowhash_load(const tcbee_frames* in_host, uint32_t rss_len, uint32_t threads,
+                        uint64_t* out_counts);
 
 /* ---- .tcp record files ----------------------------------------------------
  * Decoded TcpPacket (tcbee-process/src/bindings/tcp_packet.rs:8-28), the

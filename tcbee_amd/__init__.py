@@ -9,13 +9,14 @@ classification of raw frames, emitting TCBee's 74-byte ``*.tcp`` records
 from ._lib import (DIR_EGRESS, DIR_INGRESS, EXPORTED, F_NO_FLOWS, KEY_BYTES, LIB_PATH,
                    RECORD_BYTES, TcbeeError, device_count, lib)
 from .parser import (FLOW_DTYPE, PacketParser, ParseResult, flow_hash64, gen_frames_device,
-                     gen_frames_index_device, gen_shard_index_device, gen_shard_scratch_words)
-from .trace import Trace, splitmix64, synth_index, synth_trace
+                     gen_frames_index_device, gen_rss_load_device, gen_shard_index_device,
+                     gen_shard_scratch_words)
+from .trace import RSS_BUCKETS, Trace, rss_table, splitmix64, synth_index, synth_trace
 
 __all__ = [
     "DIR_EGRESS", "DIR_INGRESS", "EXPORTED", "F_NO_FLOWS", "KEY_BYTES", "LIB_PATH",
     "RECORD_BYTES", "TcbeeError", "device_count", "lib", "FLOW_DTYPE", "PacketParser",
     "ParseResult", "flow_hash64", "gen_frames_device", "gen_frames_index_device",
-    "gen_shard_index_device", "gen_shard_scratch_words", "Trace", "splitmix64",
-    "synth_index", "synth_trace",
+    "gen_rss_load_device", "gen_shard_index_device", "gen_shard_scratch_words", "RSS_BUCKETS",
+    "Trace", "rss_table", "splitmix64", "synth_index", "synth_trace",
 ]

@@ -174,6 +174,13 @@ _SIGS = {
                                                C.c_uint64, C.c_uint64, C.c_int, C.c_void_p,
                                                C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                                C.c_void_p]),
+    "tcbee_gen_shard_index_rss_device": (C.c_int, [C.c_uint64, C.c_int, C.c_int, C.c_int,
+                                                   C.c_uint64, C.c_uint64, C.c_int, C.c_void_p,
+                                                   C.c_uint32, C.c_void_p, C.c_void_p,
+                                                   C.c_uint64, C.c_void_p, C.c_void_p,
+                                                   C.c_void_p]),
+    "tcbee_gen_rss_load_device": (C.c_int, [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64,
+                                            C.c_uint32, C.c_void_p, C.c_void_p]),
     "tcbee_flow_hash64": (C.c_uint64, [C.c_void_p]),
     "tcbee_pipe_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(PipeCfg),
                                     C.c_uint64]),

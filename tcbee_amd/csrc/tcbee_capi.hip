@@ -1077,9 +1077,37 @@ int tcbee_gen_shard_index_device(uint64_t n_global, int world, int rank, int kin
                                  uint64_t n_flows, uint64_t seed, int imix, uint64_t* out_gidx,
                                  uint32_t* out_caplen, uint64_t cap, uint64_t* scratch,
                                  uint64_t* n_out, void* stream) {
+  return tcbee_gen_shard_index_rss_device(n_global, world, rank, kind, n_flows, seed, imix,
+                                          nullptr, 0, out_gidx, out_caplen, cap, scratch,
+                                          n_out, stream);
+}
+
+int tcbee_gen_rss_load_device(uint64_t n_frames, int kind, uint64_t n_flows, uint64_t seed,
+                              uint32_t rss_len, uint64_t* counts_dev, void* stream) {
+  if ((kind != 0 && kind != 1) || (kind == 1 && n_flows == 0) || rss_len == 0 ||
+      rss_len > kRssMaxLen || !counts_dev)
+    return TCBEE_EINVAL;
+  ShardArgs a{};
+  a.n_global = n_frames;
+  a.world = 1;
+  a.kind = kind;
+  a.n_flows = n_flows;
+  a.seed = seed;
+  a.scratch = counts_dev;
+  a.rss_len = rss_len;
+  TRY_HIP(launch_rss_load(a, (hipStream_t)stream));
+  return TCBEE_OK;
+}
+
+int tcbee_gen_shard_index_rss_device(uint64_t n_global, int world, int rank, int kind,
+                                     uint64_t n_flows, uint64_t seed, int imix,
+                                     const uint16_t* rss_dev, uint32_t rss_len,
+                                     uint64_t* out_gidx, uint32_t* out_caplen, uint64_t cap,
+                                     uint64_t* scratch, uint64_t* n_out, void* stream) {
   if (world < 1 || rank < 0 || rank >= world || (kind != 0 && kind != 1) || !scratch || !n_out ||
       (cap && (!out_gidx || !out_caplen)))
     return TCBEE_EINVAL;
+  if (rss_dev && (rss_len == 0 || rss_len > kRssMaxLen)) return TCBEE_EINVAL;
   if (kind == 1 && n_flows == 0) return TCBEE_EINVAL;
   if ((n_global + kShardChunk - 1) / kShardChunk > 0x7FFFFFFFull) return TCBEE_ECAPACITY;
   ShardArgs a{};
@@ -1095,6 +1123,8 @@ int tcbee_gen_shard_index_device(uint64_t n_global, int world, int rank, int kin
   a.cap = cap;
   a.scratch = scratch;
   a.n_out = n_out;
+  a.rss = rss_dev;
+  a.rss_len = rss_dev ? rss_len : 0;
   TRY_HIP(launch_shard_index(a, (hipStream_t)stream));
   return TCBEE_OK;
 }

@@ -288,10 +288,16 @@ struct ShardArgs {
   uint64_t cap;
   uint64_t* scratch;  // per chunk: count, then exclusive prefix
   uint64_t* n_out;
+  const uint16_t* rss;  // RSS indirection table: owner = rss[fold32 % rss_len] (NULL: % world)
+  uint32_t rss_len;
 };
+constexpr uint32_t kRssMaxLen = 4096;  // RSS table entries (LDS histogram of k_rss_load)
 constexpr int kShardPer = 16;  // global indices per thread
 constexpr uint64_t kShardChunk = 256ull * kShardPer;  // one 256-thread block (kBlock)
 hipError_t launch_shard_index(const ShardArgs& a, hipStream_t s);
+// frames per RSS bucket (fold32(flow hash) % rss_len) of global frames [0, n_global),
+// added to a.scratch[0 .. rss_len)
+hipError_t launch_rss_load(const ShardArgs& a, hipStream_t s);
 
 constexpr int kBlock = 256;
 static_assert(kShardChunk == (uint64_t)kBlock * kShardPer, "shard chunk = one block");

@@ -2820,13 +2820,19 @@ __device__ __forceinline__ uint32_t gen_caplen(uint64_t i, int imix, uint64_t se
   const uint64_t r = splitmix64((seed ^ 0x1A1Eull) + i) % 12u;
   return r < 7 ? 64u : (r < 11 ? 576u : 1500u);
 }
-// owner GPU of global frame i: its flow hash (the IpTuple K1 builds for this
-// IPv4/TCP frame, xdp.rs:116-127) folded to 32 bits, mod world
-__device__ __forceinline__ uint32_t gen_owner(const ShardArgs& a, uint64_t i) {
+// the flow hash of global frame i (the IpTuple K1 builds for this IPv4/TCP frame,
+// xdp.rs:116-127) folded to 32 bits
+__device__ __forceinline__ uint32_t gen_fold(const ShardArgs& a, uint64_t i) {
   const GenFields g = gen_fields(i, a.kind, a.n_flows, a.seed);
   const uint64_t k1 = (uint64_t)bswap32(g.saddr) << 32, k3 = (uint64_t)bswap32(g.daddr) << 32;
   const uint64_t k4 = (uint64_t)g.sport | ((uint64_t)g.dport << 16) | ((uint64_t)kTcpProtocol << 32);
-  return fold32(flow_hash64(0, k1, 0, k3, k4)) % a.world;
+  return fold32(flow_hash64(0, k1, 0, k3, k4));
+}
+// owner GPU of global frame i: the folded hash mod world, or through the RSS
+// indirection table (a NIC's receive-side scaling: hash bucket -> queue)
+__device__ __forceinline__ uint32_t gen_owner(const ShardArgs& a, uint64_t i) {
+  const uint32_t h = gen_fold(a, i);
+  return a.rss ? (uint32_t)a.rss[h % a.rss_len] : h % a.world;
 }
 
 __device__ __forceinline__ uint32_t shard_mine(const ShardArgs& a, uint64_t i0, uint32_t& bits) {
@@ -2883,6 +2889,30 @@ __global__ __launch_bounds__(kBlock) void k_shard_write(ShardArgs a) {
     }
     ++pos;
   }
+}
+
+// frames per RSS bucket: an LDS histogram per block, one device add per bucket
+__global__ __launch_bounds__(kBlock) void k_rss_load(ShardArgs a) {
+  __shared__ uint32_t s_h[kRssMaxLen];
+  for (uint32_t b = threadIdx.x; b < a.rss_len; b += kBlock) s_h[b] = 0;
+  __syncthreads();
+  for (uint64_t i = blockIdx.x * (uint64_t)kBlock + threadIdx.x; i < a.n_global;
+       i += (uint64_t)gridDim.x * kBlock)
+    atomicAdd(&s_h[gen_fold(a, i) % a.rss_len], 1u);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < a.rss_len; b += kBlock)
+    if (s_h[b]) atomicAdd((unsigned long long*)&a.scratch[b], (unsigned long long)s_h[b]);
+}
+
+hipError_t launch_rss_load(const ShardArgs& a, hipStream_t s) {
+  const hipError_t e = hipMemsetAsync(a.scratch, 0, sizeof(uint64_t) * a.rss_len, s);
+  if (e != hipSuccess) return e;
+  if (a.n_global == 0) return hipSuccess;
+  // a block covers >= 64k frames (its histogram flush costs rss_len adds)
+  uint64_t g = (a.n_global + 65535) / 65536;
+  if (g > 2048) g = 2048;
+  hipLaunchKernelGGL(k_rss_load, dim3((unsigned)g), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_shard_index(const ShardArgs& a, hipStream_t s) {

@@ -92,6 +92,9 @@ _SIGS = {
     "tcbee_tsdb_delete_attribute": (cint, [vp, i64, cstr]),
     "tcbee_metrics_write": (cint, [cstr, C.POINTER(Counters), u64, u64]),
     "tcbee_flowhash_owner": (cint, [C.POINTER(Frames), C.c_uint32, C.c_uint32, vp]),
+    "tcbee_flowhash_owner_rss": (cint, [C.POINTER(Frames), C.c_uint32, vp, C.c_uint32,
+                                        C.c_uint32, vp]),
+    "tcbee_flowhash_load": (cint, [C.POINTER(Frames), C.c_uint32, C.c_uint32, vp]),
 }
 HOST_EXPORTED = tuple(_SIGS)
 
@@ -180,19 +183,36 @@ class Pcap:
             pass
 
 
-def flowhash_owner(trace: Trace, world: int, threads: int = 8) -> np.ndarray:
+def flowhash_owner(trace: Trace, world: int, threads: int = 8, rss=None) -> np.ndarray:
     """GPU owning each frame under the flow-hash partition (tcbee_flowhash_owner:
-    the NIC-RSS step; frames the hook cannot key go round robin)."""
+    the NIC-RSS step; frames the hook cannot key go round robin). rss: an RSS
+    indirection table (uint16, entries < world; trace.rss_table) instead of
+    fold32(hash) % world (tcbee_flowhash_owner_rss)."""
     out = np.empty(max(trace.n, 1), dtype=np.uint16)
     fr = _frames_of(trace)
-    _check(hlib().tcbee_flowhash_owner(C.byref(fr), world, threads, _ptr(out)),
-           "tcbee_flowhash_owner")
+    if rss is None:
+        _check(hlib().tcbee_flowhash_owner(C.byref(fr), world, threads, _ptr(out)),
+               "tcbee_flowhash_owner")
+    else:
+        tab = np.ascontiguousarray(rss, dtype=np.uint16)
+        _check(hlib().tcbee_flowhash_owner_rss(C.byref(fr), world, _ptr(tab), len(tab), threads,
+                                               _ptr(out)), "tcbee_flowhash_owner_rss")
     return out[:trace.n]
 
 
-def flowhash_shard(trace: Trace, world: int, rank: int, threads: int = 8):
+def flowhash_load(trace: Trace, rss_len: int = 4096, threads: int = 8) -> np.ndarray:
+    """Keyed frames per RSS bucket (fold32(flow hash) % rss_len): the observed load
+    an RSS table is balanced on (tcbee_flowhash_load)."""
+    out = np.zeros(rss_len, dtype=np.uint64)
+    fr = _frames_of(trace)
+    _check(hlib().tcbee_flowhash_load(C.byref(fr), rss_len, threads, _ptr(out)),
+           "tcbee_flowhash_load")
+    return out
+
+
+def flowhash_shard(trace: Trace, world: int, rank: int, threads: int = 8, rss=None):
     """(rank's frames as a zero-copy Trace, their global frame indices)."""
-    gidx = np.nonzero(flowhash_owner(trace, world, threads) == rank)[0].astype(np.int64)
+    gidx = np.nonzero(flowhash_owner(trace, world, threads, rss) == rank)[0].astype(np.int64)
     return trace.select(gidx), gidx
 
 

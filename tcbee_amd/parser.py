@@ -315,12 +315,31 @@ def gen_frames_index_device(arena, offset, caplen, gidx, n: int, kind: int, n_fl
 
 def gen_shard_index_device(n_global: int, world: int, rank: int, kind: int, n_flows: int,
                            seed: int, imix: bool, out_gidx, out_caplen, cap: int, scratch,
-                           n_out, stream: int | None = None) -> None:
-    """Global indices + caplens of rank's flow-hash shard of the synthetic trace."""
-    _lib.check(_lib.lib().tcbee_gen_shard_index_device(
+                           n_out, stream: int | None = None, rss=None) -> None:
+    """Global indices + caplens of rank's flow-hash shard of the synthetic trace.
+    rss: an RSS indirection table on the device (uint16/int16 tensor, entries <
+    world: tcbee_gen_shard_index_rss_device), or None for fold32(hash) % world."""
+    if rss is None:
+        _lib.check(_lib.lib().tcbee_gen_shard_index_device(
+            C.c_uint64(n_global), world, rank, kind, C.c_uint64(n_flows), C.c_uint64(seed),
+            int(bool(imix)), _ptr(out_gidx), _ptr(out_caplen), C.c_uint64(cap), _ptr(scratch),
+            _ptr(n_out), C.c_void_p(stream or 0)), "tcbee_gen_shard_index_device")
+        return
+    _lib.check(_lib.lib().tcbee_gen_shard_index_rss_device(
         C.c_uint64(n_global), world, rank, kind, C.c_uint64(n_flows), C.c_uint64(seed),
-        int(bool(imix)), _ptr(out_gidx), _ptr(out_caplen), C.c_uint64(cap), _ptr(scratch),
-        _ptr(n_out), C.c_void_p(stream or 0)), "tcbee_gen_shard_index_device")
+        int(bool(imix)), _ptr(rss), C.c_uint32(int(rss.numel())), _ptr(out_gidx),
+        _ptr(out_caplen), C.c_uint64(cap), _ptr(scratch), _ptr(n_out),
+        C.c_void_p(stream or 0)), "tcbee_gen_shard_index_rss_device")
+
+
+def gen_rss_load_device(n_frames: int, kind: int, n_flows: int, seed: int, counts,
+                        stream: int | None = None) -> None:
+    """Frames per RSS bucket of global frames [0, n_frames) of the synthetic trace
+    into the int64 device tensor `counts` (its length = the table length)."""
+    _lib.check(_lib.lib().tcbee_gen_rss_load_device(
+        C.c_uint64(n_frames), kind, C.c_uint64(n_flows), C.c_uint64(seed),
+        C.c_uint32(int(counts.numel())), _ptr(counts), C.c_void_p(stream or 0)),
+        "tcbee_gen_rss_load_device")
 
 
 def gen_shard_scratch_words(n_global: int) -> int:

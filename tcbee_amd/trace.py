@@ -169,3 +169,30 @@ def synth_trace(n: int, sizes: str = "64", kind: int = GEN_SINGLE, n_flows: int 
     arena = np.zeros(arena_len + 16, dtype=np.uint8)
     gen_frames_host(arena, offset, caplen, kind, n_flows, seed, first_index)
     return Trace(arena[:arena_len] if arena_len else arena[:0], offset, caplen, ts)
+
+
+RSS_BUCKETS = 4096  # entries of the RSS indirection tables (TCBEE_RSS_MAX)
+
+
+def rss_table(load, world: int) -> np.ndarray:
+    """An RSS indirection table (NIC receive-side scaling: hash bucket -> GPU)
+    balanced on observed per-bucket frame counts: longest-processing-time greedy
+    (buckets by load, largest first, each to the least loaded GPU; ties by bucket
+    and GPU number), so every rank computes the same table from the same counts.
+    Every flow's frames share one bucket, so a flow still reaches exactly one GPU;
+    only the mapping of buckets to GPUs is chosen. uint16[len(load)]."""
+    load = np.asarray(load, dtype=np.int64)
+    if world < 1 or world > 0xFFFF or load.ndim != 1 or len(load) == 0:
+        raise ValueError("rss_table: 1 <= world <= 65535 and a non-empty 1-D load")
+    order = np.lexsort((np.arange(len(load)), -load))  # load descending, bucket ascending
+    table = np.empty(len(load), dtype=np.uint16)
+    tot = [0] * world
+    import heapq
+    heap = [(0, g) for g in range(world)]
+    for b in order:
+        t, g = heapq.heappop(heap)
+        table[b] = g
+        tot[g] = t + int(load[b])
+        heapq.heappush(heap, (tot[g], g))
+    return table
+

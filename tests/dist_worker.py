@@ -183,11 +183,16 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode, n_flows=3000, filter_po
     if fhx:
         mode = "flowhash" + mode[3:]
     gidx = None
-    if mode == "flowhash":
+    if mode in ("flowhash", "flowhash_rss"):
         import bench
         s0 = torch.cuda.current_stream().cuda_stream
+        # flowhash_rss: the bench's RSS table balanced on the bucket loads (same on
+        # every rank) instead of fold32(hash) % world
+        rss = bench.rss_for(torch, n, world, 1, n_flows, 0x7CBEE, s0)[0] if mode == "flowhash_rss" else None
         arena, alen, off, ln, ts, gidx, m = bench.build_shard_trace(
-            torch, n, world, rank, "imix", 1, n_flows, 0x7CBEE, s0)
+            torch, n, world, rank, "imix", 1, n_flows, 0x7CBEE, s0, rss=rss)
+        if rss is not None:
+            np.save(os.path.join(result_dir, f"rss{rank}.npy"), rss.cpu().numpy().view(np.uint16))
     else:
         tr = mixed_trace(n, seed=404, n_flows=n_flows)
         if mode.startswith("flowhash_"):

@@ -30,7 +30,7 @@ def test_library_loads_and_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     L = tcbee_amd.lib()
-    assert L.tcbee_abi_version() == 3
+    assert L.tcbee_abi_version() == 4
     assert L.tcbee_strerror(0) == b"ok"
     assert L.tcbee_strerror(_lib.EFLOWFULL) == b"flow table full"
     assert b"first record" in L.tcbee_strerror(_lib.ESHARD)

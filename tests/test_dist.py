@@ -120,6 +120,56 @@ def test_flowhash_owner_matches_device_shards():
         assert own[i] == ((h ^ (h >> 32)) & 0xFFFFFFFF) % 4
 
 
+def test_rss_table_lpt():
+    """rss_table: every bucket mapped to a GPU < world, deterministic, and the
+    per-GPU load within one bucket of the mean (longest-processing-time greedy)."""
+    import tcbee_amd
+    rng = np.random.default_rng(3)
+    for world in (2, 3, 8):
+        load = rng.poisson(rng.integers(0, 4, 4096) * 2000)
+        t = tcbee_amd.rss_table(load, world)
+        assert t.dtype == np.uint16 and len(t) == 4096 and int(t.max()) < world
+        assert np.array_equal(t, tcbee_amd.rss_table(load, world))
+        per = np.bincount(t, weights=load, minlength=world)
+        assert per.max() - per.mean() <= load.max()
+        assert per.max() / per.mean() < 1.001
+    with pytest.raises(ValueError):
+        tcbee_amd.rss_table([], 2)
+
+
+def test_flowhash_owner_rss_and_load(oracle):
+    """The host partitioner with an RSS table: keyed frames go to
+    table[fold32(hash) % len] (unkeyed round robin, as without a table); the bucket
+    loads count the keyed frames per bucket; a table balanced on them evens out the
+    GPUs' frame counts on a synthetic trace; bad tables are refused."""
+    import tcbee_amd
+    from tcbee_amd import host
+    from tracegen import mixed_trace
+    tr = mixed_trace(30_000, seed=11, n_flows=700)
+    fold = np.full(tr.n, -1, dtype=np.int64)
+    for i in range(tr.n):
+        key = oracle.hook(tr.frame(i))[1]
+        if key is not None:
+            h = oracle.flow_hash64(key)
+            fold[i] = (h ^ (h >> 32)) & 0xFFFFFFFF
+    keyed = fold >= 0
+    load = host.flowhash_load(tr, 512, threads=3)
+    assert np.array_equal(load, np.bincount(fold[keyed] % 512, minlength=512))
+    table = tcbee_amd.rss_table(load, 3)
+    own = host.flowhash_owner(tr, 3, threads=4, rss=table)
+    assert np.array_equal(own[keyed], table[fold[keyed] % 512])
+    assert np.array_equal(own[~keyed], (np.arange(tr.n) % 3)[~keyed])
+    syn = tcbee_amd.synth_trace(200_000, sizes="imix", kind=1, n_flows=2000)
+    t8 = tcbee_amd.rss_table(host.flowhash_load(syn, 4096), 8)
+    per = np.bincount(host.flowhash_owner(syn, 8, rss=t8), minlength=8)
+    per_mod = np.bincount(host.flowhash_owner(syn, 8), minlength=8)
+    assert per.max() / per.mean() < 1.002 < per_mod.max() / per_mod.mean()
+    with pytest.raises(tcbee_amd.TcbeeError):
+        host.flowhash_owner(tr, 2, rss=np.array([0, 1, 2], dtype=np.uint16))  # entry >= world
+    with pytest.raises(tcbee_amd.TcbeeError):
+        host.flowhash_load(tr, 4097)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_gloo_owner_exchange_mirror(oracle, tmp_path, world):
     """The owner exchange's algorithm (contiguous shards, flows merged at their hash

@@ -40,23 +40,38 @@ def test_gpu_world2_merge(gpu, oracle, tmp_path, mode):
         assert int(r["ctr"][0]) == ctr["ingress"] and int(r["ctr"][2]) == ctr["handled"]
 
 
-def test_gpu_world2_flowhash_shards(gpu, oracle, tmp_path):
+@pytest.mark.parametrize("mode", ["flowhash", "flowhash_rss", "fhx_rss"])
+def test_gpu_world2_flowhash_shards(gpu, oracle, tmp_path, mode):
     """Flow-hash shards (config 4's NIC-RSS view): each rank's frames are the
-    global frames whose flow hash % world is its rank (device shard generator);
-    records, global flow ids and the merged table vs the oracle over the global
-    trace, and the shards partition the trace."""
+    global frames whose flow hash % world is its rank (device shard generator) —
+    or, with an RSS indirection table balanced on the bucket loads (the bench's
+    N>1 placement), whose table entry is its rank; records, global flow ids and the
+    merged table vs the oracle over the global trace, and the shards partition the
+    trace."""
     import torch.multiprocessing as mp
 
     import dist_worker
     import tcbee_amd
+    from tcbee_amd import host
     from tcbee_amd.parser import FLOW_DTYPE
     n, cap, world = 120_000, 4096, 2
-    mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path), "flowhash"),
+    mp.spawn(dist_worker.run_gpu, args=(world, free_port(), n, cap, str(tmp_path), mode),
              nprocs=world, join=True)
     tr = tcbee_amd.synth_trace(n, sizes="imix", kind=1, n_flows=3000)
     rec, fh, fi, ctr, table = oracle.parse(tr)
     res = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
     owner = fh % world
+    if mode != "flowhash":
+        rss = np.load(tmp_path / "rss0.npy")
+        assert np.array_equal(rss, np.load(tmp_path / "rss1.npy"))  # one table on every rank
+        # the table is the LPT balance of the device's bucket loads, which equal the
+        # host partitioner's on the same trace; the host placement agrees frame by frame
+        load = host.flowhash_load(tr, len(rss))
+        assert np.array_equal(rss, tcbee_amd.rss_table(load, world))
+        owner = rss[fh % len(rss)]
+        assert np.array_equal(host.flowhash_owner(tr, world, rss=rss), owner)
+        per = np.bincount(owner, minlength=world)
+        assert per.max() / per.mean() < 1.01  # balanced (modulo: 3000 flows spread ~2 %)
     all_g = np.concatenate([r["gidx"] for r in res])
     assert len(all_g) == n and np.array_equal(np.sort(all_g), np.arange(n))
     for r, x in enumerate(res):

@@ -79,7 +79,7 @@ def test_host_library_exports_every_symbol():
     L = host.hlib()
     for name in host.HOST_EXPORTED:
         assert hasattr(L, name), name
-    assert L.tcbee_host_abi_version() == 1
+    assert L.tcbee_host_abi_version() == 2
     hdr = open(os.path.join(ROOT, "include", "tcbee_host.h")).read()
     for name in host.HOST_EXPORTED:
         assert name + "(" in hdr, name
