@@ -104,6 +104,11 @@ def partition_edges(rng):
     off[::50] = np.uint64(len(tr.arena) + 100)
     ln[1::50] = np.uint32(1 << 20)
     host.flowhash_owner(Trace(tr.arena, off, ln, tr.ts_ns), 5, threads=3)
+    edge = Trace(tr.arena, off, ln, tr.ts_ns)
+    load = host.flowhash_load(edge, 97, threads=3)  # RSS bucket loads, table routing
+    table = (np.arange(97) % 5).astype(np.uint16)
+    host.flowhash_owner(edge, 5, threads=3, rss=table)
+    assert int(load.sum()) <= edge.n
 
 
 def oracle_cases(rng, orc):
