@@ -325,6 +325,12 @@ def gen_shard_index_device(n_global: int, world: int, rank: int, kind: int, n_fl
             int(bool(imix)), _ptr(out_gidx), _ptr(out_caplen), C.c_uint64(cap), _ptr(scratch),
             _ptr(n_out), C.c_void_p(stream or 0)), "tcbee_gen_shard_index_device")
         return
+    import torch
+    n_rss = int(rss.numel())
+    if n_rss == 0 or n_rss > 4096 or int((rss.view(-1).to(torch.int32) & 0xFFFF).max().item()) >= world:
+        # (a table entry >= world would drop that bucket's frames on every rank: the
+        #  C ABI cannot see device memory without a copy, so the wrapper checks)
+        raise ValueError(f"RSS table: 1..4096 entries, each < world={world}")
     _lib.check(_lib.lib().tcbee_gen_shard_index_rss_device(
         C.c_uint64(n_global), world, rank, kind, C.c_uint64(n_flows), C.c_uint64(seed),
         int(bool(imix)), _ptr(rss), C.c_uint32(int(rss.numel())), _ptr(out_gidx),
