@@ -135,6 +135,11 @@ def test_rss_table_lpt():
         assert per.max() / per.mean() < 1.001
     with pytest.raises(ValueError):
         tcbee_amd.rss_table([], 2)
+    import torch
+    bad = torch.from_numpy(np.array([0, 1, 2], dtype=np.uint16).view(np.int16))
+    with pytest.raises(ValueError):  # an entry >= world would drop its bucket's frames
+        tcbee_amd.gen_shard_index_device(10, 2, 0, 1, 5, 1, True, None, None, 0, None, None,
+                                         rss=bad)
 
 
 def test_flowhash_owner_rss_and_load(oracle):
