@@ -27,6 +27,7 @@ struct tcbee_ctx {
   int k1_variant = 0;           // TCBEE_K1V: K1 staging/occupancy A/B variants
   uint32_t async_k3_blocks = 0; // TCBEE_ASYNC_K3_BLOCKS: K3 grid cap with async ids (A/B)
   uint32_t plain_walk = kPlainWalk;  // TCBEE_WALK: K1 plain probe walk length (A/B)
+  bool no_fuse_rank = false;         // TCBEE_NO_FUSE_RANK: the separate rank launch (A/B, tests)
   uint32_t pack_bits = 0;            // K1->K3 scratch packing (0: two words per record)
 
   FlowTable tab{};
@@ -261,6 +262,7 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   if (const char* e = std::getenv("TCBEE_K1V")) c->k1_variant = std::atoi(e);
   if (const char* e = std::getenv("TCBEE_ASYNC_K3_BLOCKS")) c->async_k3_blocks = (uint32_t)std::atoi(e);
   if (const char* e = std::getenv("TCBEE_WALK")) c->plain_walk = (uint32_t)std::atoi(e);
+  if (const char* e = std::getenv("TCBEE_NO_FUSE_RANK")) c->no_fuse_rank = std::atoi(e) != 0;
   if (const char* e = std::getenv("TCBEE_FPL")) {
     const int v = std::atoi(e);
     if (v == 1 || v == 2 || v == 4) c->fpl = v;
@@ -515,8 +517,16 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     // K2 rewrites claim -> id entries, zeroes new ids' counters and the bitmap K3
     // clears: after the previous batch's K3, wherever that ran
     TRY_HIP(k3_wait_stream(c, s));
-    TRY_HIP(launch_rank(r, s));
+    // a small context's batch that K2 would rank in one block: K3's blocks rank it
+    // themselves (one launch fewer per batch; config 2: 1M frames of one flow)
+    const bool fuse = r.nwords <= kRankSmallWords && c->max_flows <= kFuseRankMax && !defer &&
+                      !async && !c->no_fuse_rank;
+    if (!fuse) TRY_HIP(launch_rank(r, s));
     CountArgs k{};
+    k.fused_rank = fuse ? 1u : 0u;
+    k.new_list = c->d_new_list;
+    k.batch_rw = c->d_batch;
+    k.tab = c->tab;
     k.out_n = out_n_dev;
     k.ctr = ctr_dev;
     k.direction = cfg->direction;

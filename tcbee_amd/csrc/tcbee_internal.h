@@ -183,7 +183,16 @@ struct CountArgs {
   uint32_t chunk_off;        // 1: the two-pass scatter instead (A/B hook, TCBEE_K3ABL=91)
   uint32_t chunk;            // records per chunk: 16384 (1024 threads, one workgroup per
                              // CU) or 8192 (512 threads, two per CU; TCBEE_K3ABL=92, A/B)
+  // Fused rank (contexts of <= kFuseRankMax flows, batches K2 would rank in one
+  // block): no rank launch — every k_count block ranks the batch's new flows itself
+  // (mode 0 is certain), block 0 publishes cmap / cfs / flow_total and zeroes the new
+  // ids' counters, and k_count_reduce advances the context's bases
+  uint32_t fused_rank;
+  const uint64_t* new_list;  // (fused rank) slots first claimed this batch
+  BatchState* batch_rw;      // (fused rank) the batch state K2 would have written
+  FlowTable tab;             // (fused rank) slot fs32 words, cfs, cmap
 };
+constexpr uint64_t kFuseRankMax = 256;
 // g1 = k_count blocks; g1s = k_count_scatter blocks; g2 = k_count_bucket blocks
 // (g2 = 0: mode 1 impossible, neither is launched)
 hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned g2, hipStream_t s,

@@ -1637,6 +1637,38 @@ __device__ void count_ranges(const CountArgs& c, uint64_t n_acc, uint64_t nflows
   for (uint32_t i = tid; i < nb; i += kCountBlock) part[i] = s_bin[i];
 }
 
+// Fused rank (CountArgs::fused_rank): this batch's new flows' output ids, ranked by
+// their first records (as k_rank_small's <= kRankSortMax path), into s_map[fbase + j];
+// block 0 also publishes what K2 would have (cmap, cfs, flow_total, the clamped
+// n_new) and zeroes the new ids' counters. Returns the flow count after the batch.
+__device__ uint64_t fused_rank_block(const CountArgs& c, uint32_t* s_map) {
+  __shared__ uint32_t s_nfs[kFuseRankMax];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t base = c.persist->rec_base, fbase = c.persist->flow_count;
+  const uint64_t room = c.tab.max_claims > fbase ? c.tab.max_claims - fbase : 0;
+  const uint64_t n_new = c.batch->n_new < room ? c.batch->n_new : room;
+  for (uint32_t j = tid; j < n_new; j += kCountBlock)
+    s_nfs[j] = *slot_fs_any(c.tab, (uint32_t)c.new_list[j]);
+  __syncthreads();
+  for (uint32_t j = tid; j < n_new; j += kCountBlock) {
+    const uint32_t v = s_nfs[j];
+    uint32_t rank = 0;
+    for (uint32_t i = 0; i < n_new; ++i) rank += s_nfs[i] < v;  // broadcast reads
+    const uint32_t id = (uint32_t)(fbase + rank);
+    s_map[fbase + j] = id;
+    if (blockIdx.x == 0) {
+      c.tab.cfs[fbase + j] = base + v;  // first_seen, global record index
+      c.tab.cmap[fbase + j] = id;
+      c.tab.cnt[2ull * id] = c.tab.cnt[2ull * id + 1] = 0;
+    }
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    c.batch_rw->n_new = n_new;
+    c.batch_rw->flow_total = fbase + n_new;
+  }
+  return fbase + n_new;
+}
+
 // ABL3 (timing-only ablations, 0 in every product launch): 1 no bin updates,
 // 2 no id gather, 4 no id stores.
 // Bins are indexed by CLAIM (dense in [0, F)); the record's output id is
@@ -1648,7 +1680,8 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   __shared__ uint32_t s_map[kCountBins];  // claim index -> output id
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint64_t n_acc = c.batch->n_acc;
-  const uint64_t nflows = c.batch->flow_total;
+  // (fused rank: K2 did not run; the flow count is this block's own)
+  const uint64_t nflows = c.fused_rank ? fused_rank_block(c, s_map) : c.batch->flow_total;
   if (blockIdx.x == 0 && tid == 0) {
     // finalize (no other block reads persist in this launch)
     const uint64_t written = n_acc < c.out_cap ? n_acc : c.out_cap;
@@ -1680,9 +1713,11 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
     return;
   }
   if (mode == 0) {
+    // (fused rank: claims of this batch's new flows were mapped above)
+    const uint64_t mapped = c.fused_rank ? c.persist->flow_count : nflows;
     for (uint32_t b = tid; b < nflows; b += kCountBlock) {
       s_bin[b] = 0;
-      s_map[b] = c.omap[b];
+      if (b < mapped) s_map[b] = c.omap[b];
     }
     __syncthreads();
   }
@@ -2262,6 +2297,12 @@ __global__ __launch_bounds__(kCountBlock) void k_count_bucket(CountArgs c, uint3
 constexpr int kReduceWaves = 16;  // k_count_reduce: 1024-thread blocks
 __global__ __launch_bounds__(64 * kReduceWaves) void k_count_reduce(CountArgs c, uint32_t g1, uint32_t g2) {
   const uint64_t nflows = c.batch->flow_total;
+  if (c.fused_rank && blockIdx.x == 0 && threadIdx.x == 0) {
+    // (fused rank) the batch is classified: the bases K2 would have advanced, now
+    // that every k_count block has read the old ones
+    c.persist_rw->rec_base += c.batch->n_acc;
+    c.persist_rw->flow_count = nflows;
+  }
   const int mode = count_mode(c, nflows);
   const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;

@@ -654,3 +654,36 @@ def test_k3_chunked_scatter(gpu, oracle, variant, flows, monkeypatch):
         fl = p.flows()
         assert len(fl) == len(table) and np.array_equal(fl, table)
         assert p.status() == 0
+
+
+@pytest.mark.parametrize("fuse", [True, False])
+def test_small_context_fused_rank(gpu, oracle, monkeypatch, fuse):
+    """Contexts of <= 256 flows rank each batch's new flows inside K3 (no rank
+    launch, tcbee_capi fuse): batches of a mixed trace (both hooks' frame classes,
+    hot flows, an empty batch, a 1M-frame single-flow batch after a reset) give the
+    oracle's records, ids and table; TCBEE_NO_FUSE_RANK=1 (the separate rank
+    kernel) gives the same."""
+    from tracegen import mixed_trace
+    monkeypatch.setenv("TCBEE_NO_FUSE_RANK", "0" if fuse else "1")
+    tr = mixed_trace(80_000, seed=909, n_flows=60)
+    rec, fh, fi, ctr, table = oracle.parse(tr)
+    assert 0 < len(table) <= 256
+    with tcbee_amd.PacketParser(max_frames=1 << 20, max_arena=1 << 27, max_flows=256) as p:
+        ft = oracle.new_flowtab()
+        base = 0
+        try:
+            for lo, hi in [(0, 1), (1, 5_000), (5_000, 5_000), (5_000, 41_111), (41_111, 80_000)]:
+                part = tr.slice(lo, hi)
+                res = p.parse(part)
+                orc = oracle.parse(part, ft=ft, record_base=base)
+                assert_same(res, orc)
+                base += len(orc[0])
+            assert np.array_equal(p.flows(), oracle.flows(ft))
+            assert p.status() == 0
+        finally:
+            oracle.free_flowtab(ft)
+        one = tcbee_amd.synth_trace(1_000_000, sizes="64", kind=0, n_flows=1)
+        for _ in range(2):  # config 2, the table reset before each batch (as bench.py)
+            p.reset_flows()
+            res = p.parse(one)
+            assert_same(res, oracle.parse(one), p.flows())

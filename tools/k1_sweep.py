@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--flows-only", action="store_true", help="only the flows-on variants")
     ap.add_argument("--cap-mult", default="4", help="max_flows = mult x flows (comma list: A/B)")
     ap.add_argument("--warm", action="store_true", help="keep the flow table across steps (no reset)")
+    ap.add_argument("--min-table", type=int, default=4096, help="max_flows floor (bench.py: 64)")
     args = ap.parse_args()
     import torch
     import tcbee_amd
@@ -65,7 +66,7 @@ def main():
             if var_name:
                 os.environ[var_name] = vv
             parsers[(fpl, flows, vv, cm)] = tcbee_amd.PacketParser(
-                max_frames=n, max_flows=max(int(cm * nf), 4096))
+                max_frames=n, max_flows=max(int(cm * nf), args.min_table))
         times = {v: [] for v in variants}
         k1 = {v: [] for v in variants}
         for r in range(args.rounds):
