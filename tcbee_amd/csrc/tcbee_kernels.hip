@@ -667,7 +667,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 // ---------------------------------------------------------------------------
 // ABL: timing-only ablation bits (0 in every product launch; see tools/ablate.py)
 //   1 no look-back, 2 no record stores, 4 no header loads, 8 no index loads,
-//   16 no side outputs, 32 no first-seen competition (atomicMin)
+//   16 no side outputs, 32 no first-seen competition (atomicMin), 64 IPv4-form
+//   probes load a line of the table's first 16 MiB instead of their slot and take a
+//   hash-derived claim (what a probe served from a table small enough for the
+//   Infinity Cache would cost)
 // STAGE 0: the whole tile's records staged in LDS, stored by the block after the
 // look-back; STAGE 1: each wave stages and stores its own 64-record group per
 // round (its records are contiguous in the output), 4.7 KB of LDS per wave.
@@ -789,7 +792,8 @@ void k_parse(ParseArgs a) {
         // miss falls through to flow_upsert's coherent path.
         if (v4k[f]) {
           S0[f] = home_slot(h[f], a.tab.nlines);
-          const uint32_t l = slot_line(S0[f]), pos = S0[f] - l * kSlotsPerLine;
+          uint32_t l = slot_line(S0[f]), pos = S0[f] - l * kSlotsPerLine;
+          if (ABL & 64) l = (uint32_t)(h[f] >> 40) & ((16u << 20) / 64u - 1u);
           Q[f][0] = __builtin_amdgcn_raw_buffer_load_b128(sl_rs, l * 64u + 16u * pos, 0, PROBE_AUX);
           // (the slot and its fs32 share one 64-B half-line: the two halves of a
           //  128-B line can be of different ages in L1/L2 — a fresh published slot
@@ -822,7 +826,15 @@ void k_parse(ParseArgs a) {
           uint64_t w0 = (uint64_t)Q[f][0][0] | ((uint64_t)Q[f][0][1] << 32);
           uint64_t w1 = (uint64_t)Q[f][0][2] | ((uint64_t)Q[f][0][3] << 32);
           uint32_t fsv = FS[f];
-          for (uint32_t step = 0;; ++step) {
+          if (ABL & 64) {
+            asm volatile("" ::"v"(Q[f][0][0]), "v"(fsv));
+            sl = s;
+            cl = (uint32_t)(h[f] % a.tab.max_claims);
+            fs = 0xFFFFFFFFu;
+            slow = false;
+            w1 = 0;  // skip the walk
+          }
+          for (uint32_t step = 0; !(ABL & 64); ++step) {
             if (w1 <= kKindBusy) break;
             if ((w1 & ~kClaimBits) == kl && w0 == w0k) {  // the whole key: a hit
               sl = s;
@@ -3017,7 +3029,7 @@ static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s
     return hipGetLastError();
     switch (abl) {
       TCBEE_ABL_CASE(1) TCBEE_ABL_CASE(2) TCBEE_ABL_CASE(4) TCBEE_ABL_CASE(8)
-      TCBEE_ABL_CASE(16) TCBEE_ABL_CASE(3) TCBEE_ABL_CASE(31) TCBEE_ABL_CASE(32)
+      TCBEE_ABL_CASE(16) TCBEE_ABL_CASE(3) TCBEE_ABL_CASE(31) TCBEE_ABL_CASE(32) TCBEE_ABL_CASE(96)
       default: break;
     }
 #undef TCBEE_ABL_CASE
