@@ -1695,7 +1695,8 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   // (fused rank: K2 did not run; the flow count is this block's own)
   const uint64_t nflows = c.fused_rank ? fused_rank_block(c, s_map) : c.batch->flow_total;
   if (blockIdx.x == 0 && tid == 0) {
-    // finalize (no other block reads persist in this launch)
+    // finalize (nothing here writes what other blocks read: with a fused rank every
+    // block reads the old record base / flow count, which the reduce advances)
     const uint64_t written = n_acc < c.out_cap ? n_acc : c.out_cap;
     if (c.out_n) *c.out_n = written;
     if (c.ctr) {
