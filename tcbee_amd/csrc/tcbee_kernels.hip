@@ -169,6 +169,7 @@ __device__ __forceinline__ void load_windows(const uint8_t* __restrict__ arena, 
 #pragma unroll
         for (int c = 0; c < 5; ++c) asm volatile("s_waitcnt vmcnt(0)" : "+v"(q[f][c]) :: "memory");
     }
+    __builtin_amdgcn_s_setprio(0);  // the tile's loads are issued: back to normal priority
 #pragma unroll
     for (int f = 0; f < FPL; ++f)
 #pragma unroll
@@ -690,6 +691,9 @@ void k_parse(ParseArgs a) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint64_t tile = blockIdx.x;
   const uint64_t i0 = tile * (uint64_t)TILE;
+  // a starting wave issues its index and header loads ahead of resident waves'
+  // parse / record work (priority dropped once they are in flight, load_windows)
+  __builtin_amdgcn_s_setprio(2);
   // flows claimed before this batch (claims below it have first records in earlier
   // batches: their frames never compete for first_seen)
   const uint64_t fbase = FLOWS ? a.persist->flow_count : 0;
