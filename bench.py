@@ -67,21 +67,26 @@ RSS_WINDOW = 16_000_000  # frames of observed traffic an RSS table is balanced o
 
 def rss_for(torch, n_global, world, kind, n_flows, seed, stream):
     """The NIC's RSS indirection table (4096 hash buckets -> GPUs) balanced on the
-    bucket loads of the trace's first RSS_WINDOW frames (tcbee_gen_rss_load_device,
-    tcbee_amd.rss_table; the same table on every rank), as receive-side scaling is
-    rebalanced from observed load. Every flow still lands on one GPU. Returns the
-    table on the device and what the line reports (TCBEE_BENCH_RSS=0: None, the
-    modulo placement fold32(hash) % world)."""
+    bucket loads of RSS_WINDOW frames of the same synthetic stream OUTSIDE the
+    measured trace (global frames [n_global, n_global + RSS_WINDOW): held out, as
+    receive-side scaling is rebalanced from earlier load — ADVICE r3: balancing on
+    the measured frames made the imbalance in-sample), via
+    tcbee_gen_rss_load_range_device and tcbee_amd.rss_table; the same table on every
+    rank. Every flow still lands on one GPU. Returns the table on the device and what
+    the line reports (TCBEE_BENCH_RSS=0: None, the modulo placement
+    fold32(hash) % world); the measured imbalance is the line's shard_imbalance."""
     import tcbee_amd
     if world < 2 or os.environ.get("TCBEE_BENCH_RSS", "1") == "0":
         return None, {"rss": None}
-    win = min(n_global, RSS_WINDOW)
+    win = RSS_WINDOW
     counts = torch.empty(tcbee_amd.RSS_BUCKETS, dtype=torch.int64, device="cuda")
-    tcbee_amd.gen_rss_load_device(win, kind, n_flows, seed, counts, stream=stream)
+    tcbee_amd.gen_rss_load_device(win, kind, n_flows, seed, counts, stream=stream,
+                                  first_frame=n_global)
     load = counts.cpu().numpy()
     table = tcbee_amd.rss_table(load, world)
     per = np.bincount(table, weights=load, minlength=world)
-    info = {"rss": {"buckets": len(table), "balanced_on_frames": win,
+    info = {"rss": {"buckets": len(table), "balanced_on_frames": [n_global, n_global + win],
+                    "held_out": True,
                     "window_imbalance": round(float(per.max() / per.mean()), 5)}}
     if len(table) % world == 0:  # the modulo placement on the same window, for reference
         mod = np.bincount(np.arange(len(table)) % world, weights=load, minlength=world)
@@ -107,6 +112,8 @@ def build_shard_trace(torch, n_global, world, rank, sizes, kind, n_flows, seed, 
                                      sizes == "imix", None, None, 0, scratch, n_out,
                                      stream=stream, rss=rss)
     cap = int(n_out.item())
+    if cap < 0:  # TCBEE_RSS_INVALID: the device found a table entry >= world
+        raise RuntimeError("RSS table refused by the device (an entry >= world)")
     gidx = torch.empty(max(cap, 1), dtype=torch.int64, device="cuda")
     clen = torch.empty(max(cap, 1), dtype=torch.int32, device="cuda")
     tcbee_amd.gen_shard_index_device(n_global, world, rank, kind, n_flows, seed,

@@ -38,7 +38,8 @@
 extern "C" {
 #endif
 
-#define TCBEE_ABI_VERSION 4  /* 3: owner meta world+2 words, tcbee_status_raise_device;
+#define TCBEE_ABI_VERSION 5  /* 5: tcbee_gen_rss_load_range_device, TCBEE_RSS_INVALID;
+                              3: owner meta world+2 words, tcbee_status_raise_device;
                                 4: RSS indirection tables for the shard generator */
 
 /* ---- record / key layout constants (DESIGN.md "Data layout") ------------ */
@@ -408,7 +409,11 @@ int tcbee_gen_shard_index_device(uint64_t n_global, int world, int rank, int kin
 /* ABI 4. The same with a NIC's RSS indirection table: frame i goes to GPU
  * rss_dev[fold32(flow_hash64(key)) % rss_len] (entries < world; rss_len <= 4096;
  * rss_dev NULL = the modulo above), so a table can balance the GPUs' loads while
- * every flow still lands on exactly one GPU. */
+ * every flow still lands on exactly one GPU. The table lives in device memory, so
+ * its entries are validated on the device: a table with an entry >= world sets
+ * *n_out_dev = TCBEE_RSS_INVALID (no shard holds 2^64 - 1 frames) instead of
+ * silently dropping that bucket's frames on every rank. */
+#define TCBEE_RSS_INVALID (~(uint64_t)0)
 int tcbee_gen_shard_index_rss_device(uint64_t n_global, int world, int rank, int kind,
                                      uint64_t n_flows, uint64_t seed, int imix,
                                      const uint16_t* rss_dev, uint32_t rss_len,
@@ -420,6 +425,12 @@ int tcbee_gen_shard_index_rss_device(uint64_t n_global, int world, int rank, int
  * the observed load a table is balanced on (tcbee_amd.trace.rss_table). Asynchronous. */
 int tcbee_gen_rss_load_device(uint64_t n_frames, int kind, uint64_t n_flows, uint64_t seed,
                               uint32_t rss_len, uint64_t* counts_dev, void* stream);
+/* ABI 5. The same over global frames [first_frame, first_frame + n_frames): a table
+ * balanced on traffic outside the frames it then places (held out, as a NIC's RSS
+ * table is rebalanced from earlier load). */
+int tcbee_gen_rss_load_range_device(uint64_t first_frame, uint64_t n_frames, int kind,
+                                    uint64_t n_flows, uint64_t seed, uint32_t rss_len,
+                                    uint64_t* counts_dev, void* stream);
 
 /* ---- ingest pipeline: host frames -> records on the host ----------------
  * (replaces the live ring drain of

@@ -12,8 +12,14 @@ import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libtcbee_amd.so")
+# The variants build of the same sources (-DTCBEE_VARIANTS=1): test hooks and the
+# timing-only ablations / A/B variants selected by TCBEE_* environment variables.
+# Loaded only on request (PacketParser(variants=True): tests of those alternative
+# paths); the product library reads no environment variable.
+VARIANTS_LIB_PATH = os.path.join(_HERE, "lib", "libtcbee_amd_variants.so")
 # A/B tooling only (tools/lib_ab.sh: the same workload against an older build of the
-# kernels in another process); the product and the tests load the in-tree library
+# kernels, or the variants build, in another process); the product and the tests
+# load the in-tree library
 if os.environ.get("TCBEE_AB_LIB"):
     LIB_PATH = os.path.abspath(os.environ["TCBEE_AB_LIB"])
 
@@ -181,6 +187,9 @@ _SIGS = {
                                                    C.c_void_p]),
     "tcbee_gen_rss_load_device": (C.c_int, [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64,
                                             C.c_uint32, C.c_void_p, C.c_void_p]),
+    "tcbee_gen_rss_load_range_device": (C.c_int, [C.c_uint64, C.c_uint64, C.c_int, C.c_uint64,
+                                                  C.c_uint64, C.c_uint32, C.c_void_p,
+                                                  C.c_void_p]),
     "tcbee_flow_hash64": (C.c_uint64, [C.c_void_p]),
     "tcbee_pipe_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(PipeCfg),
                                     C.c_uint64]),
@@ -193,25 +202,27 @@ _SIGS = {
 }
 EXPORTED = tuple(_SIGS)
 
-_lib = None
+_libs: dict = {}
 
 
-def lib() -> C.CDLL:
-    """The loaded libtcbee_amd.so. Raises if it has not been built."""
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
+def lib(variants: bool = False) -> C.CDLL:
+    """The loaded libtcbee_amd.so (variants=True: libtcbee_amd_variants.so). Raises
+    if it has not been built."""
+    path = VARIANTS_LIB_PATH if variants else LIB_PATH
+    L = _libs.get(path)
+    if L is None:
+        if not os.path.exists(path):
             raise ImportError(
-                f"{LIB_PATH} is missing: build it with `make -C tcbee_amd/csrc` "
+                f"{path} is missing: build it with `make -C tcbee_amd/csrc` "
                 "or __graft_entry__.build() (no CPU fallback exists)")
         _share_hip_runtime_with_torch()
-        L = C.CDLL(LIB_PATH)
+        L = C.CDLL(path)
         for name, (res, args) in _SIGS.items():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return L
 
 
 def _share_hip_runtime_with_torch() -> None:

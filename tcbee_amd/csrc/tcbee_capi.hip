@@ -256,6 +256,10 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   c->max_frames = max_frames;
   c->max_arena = max_arena;
   c->max_flows = max_flows < 16 ? 16 : max_flows;
+#if TCBEE_VARIANTS
+  // test hooks and A/B variants, read from the environment by the variants build
+  // only (libtcbee_amd_variants.so: tests of alternative paths, tools/); the product
+  // library reads no environment variable
   if (const char* e = std::getenv("TCBEE_TEST_WITHHOLD")) c->withhold_every = (uint32_t)std::atoi(e);
   if (const char* e = std::getenv("TCBEE_TEST_K3_NOBUCKET")) c->k3_no_bucket = std::atoi(e);
   if (const char* e = std::getenv("TCBEE_K3ABL")) c->k3_variant = std::atoi(e);
@@ -267,6 +271,7 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
     const int v = std::atoi(e);
     if (v == 1 || v == 2 || v == 4) c->fpl = v;
   }
+#endif
   int rc = TCBEE_OK;
   auto fail = [&](int code) {
     tcbee_ctx_destroy(c);
@@ -287,7 +292,9 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
     uint32_t b = 1;
     while ((1ull << (b - 1)) < c->max_flows) ++b;
     c->pack_bits = b <= 21 ? b : 0;
+#if TCBEE_VARIANTS
     if (const char* e = std::getenv("TCBEE_TEST_NOPACK")) c->pack_bits = std::atoi(e) ? 0 : c->pack_bits;
+#endif
   }
   c->max_tiles = (max_frames + tile_frames(1) - 1) / tile_frames(1);
   c->max_words = (max_frames + 31) / 32;
@@ -341,7 +348,9 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   //  such tables on modes 1/2 — a test hook)
   uint64_t part_words = c->k3_g1max * kCountBins;
   c->k3_range = c->max_flows > (uint64_t)kCountBins;
+#if TCBEE_VARIANTS
   if (const char* e = std::getenv("TCBEE_TEST_K3_NORANGE")) c->k3_range = c->k3_range && !std::atoi(e);
+#endif
   if (c->k3_range) {
     const uint64_t rows = (uint64_t)c->n_cu / 2;  // R >= 2 in mode 3: <= g1/16 groups x 8
     if (rows * kRangeFlows > part_words) part_words = rows * kRangeFlows;
@@ -458,12 +467,22 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
   const uint64_t tf = tile_frames(fpl, flows && fpl == 2 ? c->k1_variant : 0);
   const uint64_t ntiles = (in->n + tf - 1) / tf;
   const uint64_t nwords = flows && ntiles ? (in->n + 31) / 32 : 0;
+  // a small context's batch that K2 would rank in one block: K3's blocks rank it
+  // themselves (one launch fewer per batch; config 2: 1M frames of one flow)
+  const bool fuse = flows && ntiles > 0 && nwords <= kRankSmallWords && c->max_flows <= kFuseRankMax &&
+                    !defer && !async && !c->no_fuse_rank;
   {
     PrepArgs pa{};
     pa.batch = c->d_batch;
     pa.tile_status = c->d_tile_status;
     pa.ntiles = ntiles;
     pa.reset = c->reset_pending;
+    if (fuse) {
+      // k_prep zeroes the counters of ids not handed out yet: after the previous
+      // batch's K3, wherever that ran
+      TRY_HIP(k3_wait_stream(c, s));
+      pa.zero_free_counters = true;
+    }
     pa.tab = c->tab;
     pa.persist = c->d_persist;
     TRY_HIP(launch_prep(pa, s));
@@ -517,10 +536,6 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     // K2 rewrites claim -> id entries, zeroes new ids' counters and the bitmap K3
     // clears: after the previous batch's K3, wherever that ran
     TRY_HIP(k3_wait_stream(c, s));
-    // a small context's batch that K2 would rank in one block: K3's blocks rank it
-    // themselves (one launch fewer per batch; config 2: 1M frames of one flow)
-    const bool fuse = r.nwords <= kRankSmallWords && c->max_flows <= kFuseRankMax && !defer &&
-                      !async && !c->no_fuse_rank;
     if (!fuse) TRY_HIP(launch_rank(r, s));
     CountArgs k{};
     k.fused_rank = fuse ? 1u : 0u;
@@ -1094,11 +1109,19 @@ int tcbee_gen_shard_index_device(uint64_t n_global, int world, int rank, int kin
 
 int tcbee_gen_rss_load_device(uint64_t n_frames, int kind, uint64_t n_flows, uint64_t seed,
                               uint32_t rss_len, uint64_t* counts_dev, void* stream) {
+  return tcbee_gen_rss_load_range_device(0, n_frames, kind, n_flows, seed, rss_len, counts_dev,
+                                         stream);
+}
+
+int tcbee_gen_rss_load_range_device(uint64_t first_frame, uint64_t n_frames, int kind,
+                                    uint64_t n_flows, uint64_t seed, uint32_t rss_len,
+                                    uint64_t* counts_dev, void* stream) {
   if ((kind != 0 && kind != 1) || (kind == 1 && n_flows == 0) || rss_len == 0 ||
       rss_len > kRssMaxLen || !counts_dev)
     return TCBEE_EINVAL;
   ShardArgs a{};
   a.n_global = n_frames;
+  a.first = first_frame;
   a.world = 1;
   a.kind = kind;
   a.n_flows = n_flows;

@@ -95,6 +95,9 @@ struct PrepArgs {
   uint64_t* tile_status;
   uint64_t ntiles;
   bool reset;           // also empty the flow table (a pending tcbee_flow_reset_device)
+  // zero the counters of every id not yet handed out (a fused-rank batch: K3's
+  // blocks add big frames to new ids' counters before any block could zero them)
+  bool zero_free_counters;
   FlowTable tab;
   PersistState* persist;
 };
@@ -299,13 +302,14 @@ struct ShardArgs {
   uint64_t* n_out;
   const uint16_t* rss;  // RSS indirection table: owner = rss[fold32 % rss_len] (NULL: % world)
   uint32_t rss_len;
+  uint64_t first;       // k_rss_load: global frames [first, first + n_global)
 };
 constexpr uint32_t kRssMaxLen = 4096;  // RSS table entries (LDS histogram of k_rss_load)
 constexpr int kShardPer = 16;  // global indices per thread
 constexpr uint64_t kShardChunk = 256ull * kShardPer;  // one 256-thread block (kBlock)
 hipError_t launch_shard_index(const ShardArgs& a, hipStream_t s);
-// frames per RSS bucket (fold32(flow hash) % rss_len) of global frames [0, n_global),
-// added to a.scratch[0 .. rss_len)
+// frames per RSS bucket (fold32(flow hash) % rss_len) of global frames
+// [first, first + n_global), into a.scratch[0 .. rss_len)
 hipError_t launch_rss_load(const ShardArgs& a, hipStream_t s);
 
 constexpr int kBlock = 256;

@@ -54,7 +54,7 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 
 constexpr uint32_t kSpinLimit = 1u << 24;
 constexpr uint32_t kRecountSpins = 4096;  // ~0.1 ms of polling before recounting
-constexpr int kAuxSc1 = 16;   // buffer cache-policy bits: sc1 (agent coherence, bypass L1)
+[[maybe_unused]] constexpr int kAuxSc1 = 16;  // buffer cache-policy bits: sc1 (agent coherence, bypass L1)
 constexpr int kAuxPlain = 0;  // plain: L1/L2 allocating
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -137,6 +137,7 @@ __device__ __forceinline__ void load_windows(const uint8_t* __restrict__ arena, 
         put_chunk(w[f], c, v);
       }
     }
+    __builtin_amdgcn_s_setprio(0);
     return;
   }
   bool inb = true;
@@ -186,6 +187,7 @@ __device__ __forceinline__ void load_windows(const uint8_t* __restrict__ arena, 
         put_chunk(w[f], c, v);
       }
     }
+    __builtin_amdgcn_s_setprio(0);  // (a window at the arena end: bounded loads, done)
   }
 }
 
@@ -1048,6 +1050,11 @@ __global__ void k_prep(PrepArgs p) {
     // (wide slots only once a non-IPv4 key was claimed)
     empty_units(p.tab, t0, stride);
   }
+  if (p.zero_free_counters) {
+    // (ordered after the previous batch's K3 by the caller; <= kFuseRankMax ids)
+    const uint64_t fbase = p.reset ? 0 : p.persist->flow_count;
+    for (uint64_t i = 2 * fbase + t0; i < 2 * p.tab.max_claims; i += stride) p.tab.cnt[i] = 0;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1656,7 +1663,9 @@ __device__ void count_ranges(const CountArgs& c, uint64_t n_acc, uint64_t nflows
 // Fused rank (CountArgs::fused_rank): this batch's new flows' output ids, ranked by
 // their first records (as k_rank_small's <= kRankSortMax path), into s_map[fbase + j];
 // block 0 also publishes what K2 would have (cmap, cfs, flow_total, the clamped
-// n_new) and zeroes the new ids' counters. Returns the flow count after the batch.
+// n_new). The new ids' counters were zeroed by k_prep (zero_free_counters): every
+// block may add a big frame to them, and nothing orders those adds after a zeroing
+// here. Returns the flow count after the batch.
 __device__ uint64_t fused_rank_block(const CountArgs& c, uint32_t* s_map) {
   __shared__ uint32_t s_nfs[kFuseRankMax];
   const uint32_t tid = threadIdx.x;
@@ -1675,7 +1684,6 @@ __device__ uint64_t fused_rank_block(const CountArgs& c, uint32_t* s_map) {
     if (blockIdx.x == 0) {
       c.tab.cfs[fbase + j] = base + v;  // first_seen, global record index
       c.tab.cmap[fbase + j] = id;
-      c.tab.cnt[2ull * id] = c.tab.cnt[2ull * id + 1] = 0;
     }
   }
   if (blockIdx.x == 0 && tid == 0) {
@@ -1738,9 +1746,11 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
     }
     __syncthreads();
   }
-  // counters are kept by LOCAL dense id
+  // counters are kept by LOCAL dense id (fused rank: omap is the local map and
+  // s_map holds it — block 0's cmap stores for this batch's new flows are not
+  // ordered before other blocks' reads)
   auto global_add = [&](uint32_t claim, uint64_t pk, uint64_t by) {
-    const uint32_t lid = c.cmap[claim];
+    const uint32_t lid = c.fused_rank ? s_map[claim] : c.cmap[claim];
     atomicAdd((unsigned long long*)&c.cnt[2ull * lid], (unsigned long long)pk);
     atomicAdd((unsigned long long*)&c.cnt[2ull * lid + 1], (unsigned long long)by);
   };
@@ -2915,11 +2925,19 @@ __global__ __launch_bounds__(kBlock) void k_shard_count(ShardArgs a) {
 // one block: exclusive prefix over the chunk counts (each thread a contiguous run)
 __global__ __launch_bounds__(kBlock) void k_shard_scan(ShardArgs a, uint64_t nchunks) {
   __shared__ uint64_t s_sum[kBlock];
+  __shared__ uint32_t s_bad;
   const uint64_t per = (nchunks + kBlock - 1) / kBlock;
   const uint64_t lo = threadIdx.x * per, hi = lo + per < nchunks ? lo + per : nchunks;
   uint64_t sum = 0;
   for (uint64_t b = lo; b < hi; ++b) sum += a.scratch[b];
   s_sum[threadIdx.x] = sum;
+  if (threadIdx.x == 0) s_bad = 0;
+  __syncthreads();
+  // an RSS entry >= world would drop its bucket's frames on every rank: such a
+  // table yields the count ~0 (TCBEE_RSS_INVALID), which no shard can have
+  if (a.rss)
+    for (uint32_t b = threadIdx.x; b < a.rss_len; b += kBlock)
+      if ((uint32_t)a.rss[b] >= (uint32_t)a.world) s_bad = 1;
   __syncthreads();
   uint64_t base = 0;
   for (uint32_t t = 0; t < threadIdx.x; ++t) base += s_sum[t];
@@ -2928,7 +2946,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_scan(ShardArgs a, uint64_t nch
     a.scratch[b] = base;
     base += c;
   }
-  if (threadIdx.x == kBlock - 1) *a.n_out = base;
+  if (threadIdx.x == kBlock - 1) *a.n_out = s_bad ? ~0ull : base;
 }
 
 __global__ __launch_bounds__(kBlock) void k_shard_write(ShardArgs a) {
@@ -2956,7 +2974,7 @@ __global__ __launch_bounds__(kBlock) void k_rss_load(ShardArgs a) {
   __syncthreads();
   for (uint64_t i = blockIdx.x * (uint64_t)kBlock + threadIdx.x; i < a.n_global;
        i += (uint64_t)gridDim.x * kBlock)
-    atomicAdd(&s_h[gen_fold(a, i) % a.rss_len], 1u);
+    atomicAdd(&s_h[gen_fold(a, a.first + i) % a.rss_len], 1u);
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < a.rss_len; b += kBlock)
     if (s_h[b]) atomicAdd((unsigned long long*)&a.scratch[b], (unsigned long long)s_h[b]);
@@ -2995,29 +3013,29 @@ hipError_t launch_table_init(FlowTable t, hipStream_t s) {
   return hipGetLastError();
 }
 
+#if TCBEE_VARIANTS
+// k1v (TCBEE_K1V at context creation) and the TCBEE_PROBE_AUX / TCBEE_ABLATE /
+// TCBEE_STAGE / TCBEE_NT environment: staging, occupancy, cache-policy A/B variants
+// and timing-only ablations (several write wrong records on purpose). Returns true
+// when it launched a variant.
 template <int FPL>
-static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s, int k1v) {
-  const dim3 grid((unsigned)a.ntiles);
-  // k1v (TCBEE_K1V at context creation): staging / occupancy A/B variants
+static bool launch_parse_variant(const ParseArgs& a, bool flows, hipStream_t s, int k1v, dim3 grid) {
   if constexpr (FPL == 2) if (flows && k1v) {
     switch (k1v) {
-      case 1: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 0>), grid, dim3(kBlock), 0, s, a); break;
-      case 2: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 5>), grid, dim3(kBlock), 0, s, a); break;
-      case 3: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 6>), grid, dim3(kBlock), 0, s, a); break;
-      // 512-thread tiles (1024 frames): half the tiles and look-back hops (A/B;
-      // the context sizes ntiles for it: k1_tile_blocks)
-      case 20: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 0, false, 0, 0, 512>), grid, dim3(512), 0, s, a); break;
+      case 1: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 0>), grid, dim3(kBlock), 0, s, a); return true;
+      case 2: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 5>), grid, dim3(kBlock), 0, s, a); return true;
+      case 3: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 6>), grid, dim3(kBlock), 0, s, a); return true;
+      // 512-thread tiles (1024 frames): half the tiles and look-back hops (the
+      // context sizes ntiles for it: k1_tile_blocks)
+      case 20: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 0, false, 0, 0, 512>), grid, dim3(512), 0, s, a); return true;
 #define TCBEE_HPOL_CASE(P) \
-      case 10 + P: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 0, false, 0, P>), grid, dim3(kBlock), 0, s, a); break;
+      case 10 + P: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 0, false, 0, P>), grid, dim3(kBlock), 0, s, a); return true;
       TCBEE_HPOL_CASE(1) TCBEE_HPOL_CASE(2) TCBEE_HPOL_CASE(3) TCBEE_HPOL_CASE(4) TCBEE_HPOL_CASE(5)
       TCBEE_HPOL_CASE(6)
 #undef TCBEE_HPOL_CASE
-      default: return hipErrorInvalidValue;
+      default: return false;
     }
-    return hipGetLastError();
   }
-  // probe-load cache policy: plain (L1/L2-allocating) by default; TCBEE_PROBE_AUX=16
-  // selects sc1 (agent-coherent, bypasses L1) for A/B runs
   static const int aux = [] {
     const char* e = getenv("TCBEE_PROBE_AUX");
     return e ? atoi(e) : kAuxPlain;
@@ -3031,7 +3049,7 @@ static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s
   case B:                                                                                      \
     if (flows) hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, B>), grid, dim3(kBlock), 0, s, a); \
     else hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain, B>), grid, dim3(kBlock), 0, s, a);     \
-    return hipGetLastError();
+    return true;
     switch (abl) {
       TCBEE_ABL_CASE(1) TCBEE_ABL_CASE(2) TCBEE_ABL_CASE(4) TCBEE_ABL_CASE(8)
       TCBEE_ABL_CASE(16) TCBEE_ABL_CASE(3) TCBEE_ABL_CASE(31) TCBEE_ABL_CASE(32) TCBEE_ABL_CASE(96)
@@ -3046,7 +3064,7 @@ static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s
   if (stage == 1) {
     if (flows) hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1>), grid, dim3(kBlock), 0, s, a);
     else hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain, 0, 1>), grid, dim3(kBlock), 0, s, a);
-    return hipGetLastError();
+    return true;
   }
   static const int nt = [] {
     const char* e = getenv("TCBEE_NT");
@@ -3055,14 +3073,28 @@ static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s
   if (nt) {
     if (flows) hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 0, true>), grid, dim3(kBlock), 0, s, a);
     else hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain, 0, 0, true>), grid, dim3(kBlock), 0, s, a);
-    return hipGetLastError();
+    return true;
   }
-  if (flows) {
-    if (aux == kAuxSc1) hipLaunchKernelGGL((k_parse<FPL, true, kAuxSc1>), grid, dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain>), grid, dim3(kBlock), 0, s, a);
-  } else {
-    hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain>), grid, dim3(kBlock), 0, s, a);
+  if (flows && aux == kAuxSc1) {
+    hipLaunchKernelGGL((k_parse<FPL, true, kAuxSc1>), grid, dim3(kBlock), 0, s, a);
+    return true;
   }
+  return false;
+}
+#endif
+
+template <int FPL>
+static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s, int k1v) {
+  const dim3 grid((unsigned)a.ntiles);
+#if TCBEE_VARIANTS
+  // timing-only ablations and A/B variants: the variants build only
+  // (libtcbee_amd_variants.so); the product library has no such dispatch
+  if (launch_parse_variant<FPL>(a, flows, s, k1v, grid)) return hipGetLastError();
+#else
+  (void)k1v;
+#endif
+  if (flows) hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain>), grid, dim3(kBlock), 0, s, a);
+  else hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain>), grid, dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
@@ -3098,8 +3130,9 @@ hipError_t launch_rank(const RankArgs& r, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned g2, hipStream_t s,
-                        int k3v) {
+#if TCBEE_VARIANTS
+static void launch_count_variant(const CountArgs& c, unsigned g1, unsigned g1s, unsigned g2,
+                                 hipStream_t s, int k3v) {
   const dim3 grid(g1);
   // k3v (TCBEE_K3ABL at context creation): timing-only ablation / tiling A/B
 #define KC(U, A)                                                                     \
@@ -3166,6 +3199,44 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
     }
     hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1s);
   }
+}
+#endif
+
+hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned g2, hipStream_t s,
+                        int k3v) {
+#if TCBEE_VARIANTS
+  // k3v (TCBEE_K3ABL at context creation): timing-only ablations / tiling A/B —
+  // the variants build only
+  launch_count_variant(c, g1, g1s, g2, s, k3v);
+#else
+  (void)k3v;
+  const dim3 grid(g1);
+  if (c.pack_bits) hipLaunchKernelGGL((k_count<8, 0, true>), grid, dim3(kCountBlock), 0, s, c);
+  else hipLaunchKernelGGL((k_count<8, 0, false>), grid, dim3(kCountBlock), 0, s, c);
+  // the two-pass scatter only where the chunked one may not cover a batch (tables
+  // of >= kChunkMaxNb buckets): no empty launches otherwise
+  const bool two_pass = !c.coffs || c.nb_max >= kChunkMaxNb;
+  if (g2 && two_pass) {
+    const dim3 gs(g1s);
+    // (each of the two returns at once unless the batch's bucket count is its own)
+    if (c.pack_bits) {
+      hipLaunchKernelGGL((k_count_scatter<8, true>), gs, dim3(kCountBlock), 0, s, c);
+      hipLaunchKernelGGL((k_count_scatter_staged<4, true>), gs, dim3(kCountBlock), 0, s, c);
+    } else {
+      hipLaunchKernelGGL((k_count_scatter<8, false>), gs, dim3(kCountBlock), 0, s, c);
+      hipLaunchKernelGGL((k_count_scatter_staged<4, false>), gs, dim3(kCountBlock), 0, s, c);
+    }
+  }
+  if (g2) {
+    if (c.coffs) {
+      // 12288-record chunks in 76 KiB of LDS: two 512-thread workgroups per CU
+      const dim3 gc(g1s ? g1s : 1);
+      if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk2<true, 512, 24>), gc, dim3(512), 0, s, c);
+      else hipLaunchKernelGGL((k_count_chunk2<false, 512, 24>), gc, dim3(512), 0, s, c);
+    }
+    hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1s);
+  }
+#endif
   // mode 0 needs kCountBins threads; mode 1 up to nb_max * kBucket (grid-stride)
   // (1024-thread blocks: mode 0 takes 64 claims per block, its 16 waves split the rows)
   const unsigned gr = (g2 || c.range_ok) ? 256u : (unsigned)(kCountBins / 256);
@@ -3274,13 +3345,17 @@ hipError_t launch_merge(const MergeArgs& g, const RankArgs& r, hipStream_t s) {
 
 hipError_t launch_remap(uint32_t* ids, uint64_t n_max, const uint64_t* n_dev, const uint32_t* map,
                         uint64_t map_len, hipStream_t s) {
-  // up to 512 workgroups (TCBEE_REMAP_GRID: A/B; beside the next step's K1,
-  // 32..512 workgroups gave the same step time once the LDS map was u16)
+  // up to 512 workgroups (beside the next step's K1, 32..512 workgroups gave the
+  // same step time once the LDS map was u16: TCBEE_REMAP_GRID, variants build)
+#if TCBEE_VARIANTS
   static const uint64_t gmax = [] {
     const char* e = getenv("TCBEE_REMAP_GRID");
     const long long v = e ? atoll(e) : 0;
     return v > 0 ? (uint64_t)v : 512ull;  // unset, 0 or garbage: the default
   }();
+#else
+  constexpr uint64_t gmax = 512;
+#endif
   const uint64_t want = (n_max + 4ull * kRemapBlock - 1) / (4ull * kRemapBlock);
   hipLaunchKernelGGL(k_remap, dim3((unsigned)(want < gmax ? (want ? want : 1) : gmax)),
                      dim3(kRemapBlock), 0, s, ids, n_max, n_dev, map,

@@ -401,8 +401,11 @@ int tcbee_pipe_create(tcbee_pipe** out, int device, const tcbee_pipe_cfg* pc,
   if (!p) return TCBEE_ENOMEM;
   p->device = device;
   p->cfg = c;
+#if TCBEE_VARIANTS
+  // gather prefetch distance / streaming copies (A/B, variants build only)
   if (const char* e = std::getenv("TCBEE_PIPE_PF")) p->prefetch = std::strtoull(e, nullptr, 10);
   if (const char* e = std::getenv("TCBEE_PIPE_NT")) p->nt_copy = std::atoi(e);
+#endif
   int rc = tcbee_ctx_create(&p->ctx, device, c.chunk_frames, 0, max_flows ? max_flows : 1 << 20);
   if (rc) return free_pipe(p), rc;
   void* cs = nullptr;
@@ -417,7 +420,9 @@ int tcbee_pipe_create(tcbee_pipe** out, int device, const tcbee_pipe_cfg* pc,
     // `threads` in all: a quarter copy records out while the rest gather
     // (TCBEE_PIPE_CTHREADS: the copy-out share, A/B)
     unsigned ct = c.threads >= 4 ? c.threads / 4 : 1;
+#if TCBEE_VARIANTS
     if (const char* e = std::getenv("TCBEE_PIPE_CTHREADS")) ct = (unsigned)std::atoi(e);
+#endif
     if (ct < 1) ct = 1;
     const unsigned gt = c.threads > ct ? c.threads - ct : 1;
     p->pool = new Pool(gt);

@@ -52,8 +52,13 @@ def _ptr(x) -> int:
 
 class PacketParser:
     def __init__(self, device: int = 0, max_frames: int = 1 << 20, max_arena: int = 0,
-                 max_flows: int = 1 << 16):
-        L = _lib.lib()
+                 max_flows: int = 1 << 16, variants: bool = False):
+        """variants=True: a context of the variants build (libtcbee_amd_variants.so),
+        whose test hooks / A/B variants follow TCBEE_* environment variables read at
+        creation — for tests of those alternative paths; the product library ignores
+        the environment."""
+        L = _lib.lib(variants)
+        self._L = L
         h = C.c_void_p()
         _lib.check(L.tcbee_ctx_create(C.byref(h), device, C.c_uint64(max_frames),
                                       C.c_uint64(max_arena), C.c_uint64(max_flows)),
@@ -66,10 +71,12 @@ class PacketParser:
         self.max_flows = max_flows
 
     @classmethod
-    def _borrow(cls, handle: C.c_void_p, device: int, max_frames: int, max_flows: int):
-        """A non-owning view of a context owned elsewhere (e.g. an ingest pipeline)."""
+    def _borrow(cls, handle: C.c_void_p, device: int, max_frames: int, max_flows: int,
+                lib: C.CDLL | None = None):
+        """A non-owning view of a context owned elsewhere (e.g. an ingest pipeline;
+        `lib`: the library that created it)."""
         self = cls.__new__(cls)
-        self._h, self._owned = handle, False
+        self._h, self._owned, self._L = handle, False, lib or _lib.lib()
         self.device, self.max_frames, self.max_arena, self.max_flows = (device, max_frames, 0,
                                                                         max_flows)
         return self
@@ -78,7 +85,7 @@ class PacketParser:
     def close(self) -> None:
         if self._h:
             if self._owned:
-                _lib.lib().tcbee_ctx_destroy(self._h)
+                self._L.tcbee_ctx_destroy(self._h)
             self._h = None
 
     def __enter__(self):
@@ -96,15 +103,15 @@ class PacketParser:
     @property
     def stream(self) -> int:
         s = C.c_void_p()
-        _lib.check(_lib.lib().tcbee_ctx_stream(self._h, C.byref(s)), "tcbee_ctx_stream")
+        _lib.check(self._L.tcbee_ctx_stream(self._h, C.byref(s)), "tcbee_ctx_stream")
         return s.value or 0
 
     def sync(self) -> None:
-        _lib.check(_lib.lib().tcbee_ctx_sync(self._h), "tcbee_ctx_sync")
+        _lib.check(self._L.tcbee_ctx_sync(self._h), "tcbee_ctx_sync")
 
     def status(self) -> int:
         """Sticky in-kernel status since the last call (OK / EFLOWFULL / ESPIN)."""
-        return _lib.lib().tcbee_ctx_status(self._h)
+        return self._L.tcbee_ctx_status(self._h)
 
     # -- host-pointer path ---------------------------------------------------
     def parse(self, trace: Trace, filter_port: int = 0, direction: int = _lib.DIR_INGRESS,
@@ -121,7 +128,7 @@ class PacketParser:
         cfg = _lib.Cfg(filter_port, direction, 0, 0 if flows else _lib.F_NO_FLOWS)
         nout = C.c_uint64(0)
         ctr = _lib.Counters()
-        _lib.check(_lib.lib().tcbee_parse_batch(
+        _lib.check(self._L.tcbee_parse_batch(
             self._h, C.byref(fr), C.byref(cfg), rec.ctypes.data, C.c_uint64(cap),
             _ptr(fh), _ptr(fi), C.byref(nout), C.byref(ctr)), "tcbee_parse_batch")
         k = nout.value
@@ -145,46 +152,46 @@ class PacketParser:
         fr = _lib.Frames(_ptr(arena), arena_len, _ptr(offset), _ptr(caplen), _ptr(ts_ns), n)
         cfg = _lib.Cfg(filter_port, direction, 0, 0 if flows else _lib.F_NO_FLOWS)
         if out_frame is None and not defer_ids and not ids_stream:
-            _lib.check(_lib.lib().tcbee_parse_batch_device(
+            _lib.check(self._L.tcbee_parse_batch_device(
                 self._h, C.byref(fr), C.byref(cfg), _ptr(out_rec), C.c_uint64(out_cap),
                 _ptr(out_hash), _ptr(out_id), _ptr(out_n), _ptr(counters),
                 C.c_void_p(stream or 0)), "tcbee_parse_batch_device")
             return
         ex = _lib.ParseEx(_ptr(out_frame), (_lib.EX_DEFER_IDS if defer_ids else 0)
                           | (_lib.EX_ASYNC_IDS if ids_stream else 0), 0, ids_stream or None)
-        _lib.check(_lib.lib().tcbee_parse_batch_device_ex(
+        _lib.check(self._L.tcbee_parse_batch_device_ex(
             self._h, C.byref(fr), C.byref(cfg), _ptr(out_rec), C.c_uint64(out_cap),
             _ptr(out_hash), _ptr(out_id), _ptr(out_n), _ptr(counters), C.byref(ex),
             C.c_void_p(stream or 0)), "tcbee_parse_batch_device_ex")
 
     def finish_device(self, id_map=None, map_len: int = 0, stream: int | None = None) -> None:
         """K3 of a defer_ids parse: out_id = id_map[local id] (or the local id)."""
-        _lib.check(_lib.lib().tcbee_parse_finish_device(
+        _lib.check(self._L.tcbee_parse_finish_device(
             self._h, _ptr(id_map), C.c_uint64(map_len if id_map is not None else 0),
             C.c_void_p(stream or 0)), "tcbee_parse_finish_device")
 
     def count_mode(self) -> int:
         """K3 mode of the last batch (0 bins, 1 buckets, 2 atomics, 3 claim ranges)."""
         m = C.c_int(-1)
-        _lib.check(_lib.lib().tcbee_ctx_count_mode(self._h, C.byref(m)), "tcbee_ctx_count_mode")
+        _lib.check(self._L.tcbee_ctx_count_mode(self._h, C.byref(m)), "tcbee_ctx_count_mode")
         return m.value
 
     # -- measurement --------------------------------------------------------------
     def profile(self, enable: bool = True) -> None:
-        _lib.check(_lib.lib().tcbee_ctx_profile(self._h, int(enable)), "tcbee_ctx_profile")
+        _lib.check(self._L.tcbee_ctx_profile(self._h, int(enable)), "tcbee_ctx_profile")
 
     def profile_read(self):
         """(summed K1 ms, K1 launches) since profile(True)."""
         ms = C.c_double(0)
         k = C.c_uint64(0)
-        _lib.check(_lib.lib().tcbee_ctx_profile_read(self._h, C.byref(ms), C.byref(k)),
+        _lib.check(self._L.tcbee_ctx_profile_read(self._h, C.byref(ms), C.byref(k)),
                    "tcbee_ctx_profile_read")
         return ms.value, k.value
 
     # -- flow table -------------------------------------------------------------
     def flow_count(self) -> int:
         n = C.c_uint64(0)
-        _lib.check(_lib.lib().tcbee_flow_count(self._h, C.byref(n)), "tcbee_flow_count")
+        _lib.check(self._L.tcbee_flow_count(self._h, C.byref(n)), "tcbee_flow_count")
         return n.value
 
     def flows(self) -> np.ndarray:
@@ -192,22 +199,22 @@ class PacketParser:
         cnt = self.flow_count()
         out = np.zeros(max(cnt, 1), dtype=FLOW_DTYPE)
         n = C.c_uint64(0)
-        _lib.check(_lib.lib().tcbee_flow_export(self._h, out.ctypes.data, C.c_uint64(cnt),
+        _lib.check(self._L.tcbee_flow_export(self._h, out.ctypes.data, C.c_uint64(cnt),
                                                 C.byref(n)), "tcbee_flow_export")
         return out[:n.value]
 
     def reset_flows(self, stream: int | None = None, sync: bool = True) -> None:
         if sync:
-            _lib.check(_lib.lib().tcbee_flow_reset(self._h), "tcbee_flow_reset")
+            _lib.check(self._L.tcbee_flow_reset(self._h), "tcbee_flow_reset")
         else:
-            _lib.check(_lib.lib().tcbee_flow_reset_device(self._h, C.c_void_p(stream or 0)),
+            _lib.check(self._L.tcbee_flow_reset_device(self._h, C.c_void_p(stream or 0)),
                        "tcbee_flow_reset_device")
 
     # -- device-side flow tables (multi-GPU merge) ---------------
     def export_device(self, out, cap: int, meta=None, stream: int | None = None) -> None:
         """out[id] = flow entry (u64[8]) for ids < cap; meta (device u64[2]) receives
         {flows exported, accepted frames so far}. Asynchronous."""
-        _lib.check(_lib.lib().tcbee_flow_export_device(
+        _lib.check(self._L.tcbee_flow_export_device(
             self._h, _ptr(out), C.c_uint64(cap), _ptr(meta), C.c_void_p(stream or 0)),
             "tcbee_flow_export_device")
 
@@ -217,7 +224,7 @@ class PacketParser:
         """As export_device, first_seen = global frame index of each flow's first
         record (frame_gidx[rec_frame[r]], or frame_gidx[r] when every frame was
         accepted); meta[1] = 0. The table must hold one batch's flows."""
-        _lib.check(_lib.lib().tcbee_flow_export_global_device(
+        _lib.check(self._L.tcbee_flow_export_global_device(
             self._h, _ptr(out), C.c_uint64(cap), _ptr(meta), _ptr(rec_frame), _ptr(frame_gidx),
             C.c_uint64(n_frames), C.c_uint64(rec_frame_cap), C.c_void_p(stream or 0)),
             "tcbee_flow_export_global_device")
@@ -228,7 +235,7 @@ class PacketParser:
         """For the flows first seen in the last batch (local ids fbase..): out[id -
         fbase] = global frame index of the flow's first record; n_dev = {n_new,
         fbase} (the flow-hash exchange's per-rank input)."""
-        _lib.check(_lib.lib().tcbee_flow_first_frames_device(
+        _lib.check(self._L.tcbee_flow_first_frames_device(
             self._h, _ptr(out), C.c_uint64(cap), _ptr(n_dev), _ptr(rec_frame), _ptr(frame_gidx),
             C.c_uint64(n_frames), C.c_uint64(rec_frame_cap), C.c_void_p(stream or 0)),
             "tcbee_flow_first_frames_device")
@@ -237,13 +244,13 @@ class PacketParser:
                               out_counts, cap: int, stream: int | None = None) -> None:
         """out_counts[id] = this rank's records whose global frame index is below
         merged flow id's first_seen (a global frame index)."""
-        _lib.check(_lib.lib().tcbee_flow_records_before_device(
+        _lib.check(self._L.tcbee_flow_records_before_device(
             self._h, _ptr(rec_frame), _ptr(frame_gidx), _ptr(n_rec_dev), C.c_uint64(n_rec_max),
             _ptr(out_counts), C.c_uint64(cap), C.c_void_p(stream or 0)),
             "tcbee_flow_records_before_device")
 
     def set_first_seen_device(self, fs_by_id, cap: int, stream: int | None = None) -> None:
-        _lib.check(_lib.lib().tcbee_flow_set_first_seen_device(
+        _lib.check(self._L.tcbee_flow_set_first_seen_device(
             self._h, _ptr(fs_by_id), C.c_uint64(cap), C.c_void_p(stream or 0)),
             "tcbee_flow_set_first_seen_device")
 
@@ -254,7 +261,7 @@ class PacketParser:
         records, entries dropped}."""
         if meta.numel() < world + 2:
             raise ValueError(f"owner meta needs world + 2 = {world + 2} words")
-        _lib.check(_lib.lib().tcbee_owner_bucket_device(
+        _lib.check(self._L.tcbee_owner_bucket_device(
             self._h, world, C.c_uint64(seg_cap), C.c_uint64(map_cap), _ptr(ent), _ptr(lid),
             _ptr(meta),
             C.c_void_p(stream or 0)), "tcbee_owner_bucket_device")
@@ -262,20 +269,20 @@ class PacketParser:
     def status_raise_device(self, v, n: int, stride: int, stream: int | None = None) -> None:
         """TCBEE_ESHARD on this context if any v[i * stride] (i < n, device u64) is
         non-zero: a peer's dropped owner entries (OwnerExchange)."""
-        _lib.check(_lib.lib().tcbee_status_raise_device(
+        _lib.check(self._L.tcbee_status_raise_device(
             self._h, _ptr(v), C.c_uint64(n), C.c_uint64(stride), C.c_void_p(stream or 0)),
             "tcbee_status_raise_device")
 
     def first_seen_device(self, out, cap: int, n_dev, stream: int | None = None) -> None:
         """out[id] = first_seen of flow id (ascending in id); n_dev = {flows, 0}."""
-        _lib.check(_lib.lib().tcbee_flow_first_seen_device(
+        _lib.check(self._L.tcbee_flow_first_seen_device(
             self._h, _ptr(out), C.c_uint64(cap), _ptr(n_dev), C.c_void_p(stream or 0)),
             "tcbee_flow_first_seen_device")
 
     def merge_device(self, entries, nseg: int, stride: int, seg_meta, max_total_records: int,
                      out_ids, stream: int | None = None) -> None:
         """Replace this context's table by the merge of nseg exported tables."""
-        _lib.check(_lib.lib().tcbee_flow_merge_device(
+        _lib.check(self._L.tcbee_flow_merge_device(
             self._h, _ptr(entries), C.c_uint64(nseg), C.c_uint64(stride), _ptr(seg_meta),
             C.c_uint64(max_total_records), _ptr(out_ids), C.c_void_p(stream or 0)),
             "tcbee_flow_merge_device")
@@ -318,7 +325,9 @@ def gen_shard_index_device(n_global: int, world: int, rank: int, kind: int, n_fl
                            n_out, stream: int | None = None, rss=None) -> None:
     """Global indices + caplens of rank's flow-hash shard of the synthetic trace.
     rss: an RSS indirection table on the device (uint16/int16 tensor, entries <
-    world: tcbee_gen_shard_index_rss_device), or None for fold32(hash) % world."""
+    world: tcbee_gen_shard_index_rss_device), or None for fold32(hash) % world.
+    n_out receives TCBEE_RSS_INVALID (~0; -1 in an int64 tensor) for a table the
+    device finds an entry >= world in."""
     if rss is None:
         _lib.check(_lib.lib().tcbee_gen_shard_index_device(
             C.c_uint64(n_global), world, rank, kind, C.c_uint64(n_flows), C.c_uint64(seed),
@@ -326,6 +335,10 @@ def gen_shard_index_device(n_global: int, world: int, rank: int, kind: int, n_fl
             _ptr(n_out), C.c_void_p(stream or 0)), "tcbee_gen_shard_index_device")
         return
     import torch
+    if rss.dtype not in (torch.int16, torch.uint16) or not rss.is_cuda or not rss.is_contiguous():
+        # (the kernel reads the table as contiguous u16 words in device memory: an
+        #  int32/int64 table would be read as interleaved zeros — ADVICE r3)
+        raise ValueError("RSS table: a contiguous int16/uint16 device tensor")
     n_rss = int(rss.numel())
     if n_rss == 0 or n_rss > 4096 or int((rss.view(-1).to(torch.int32) & 0xFFFF).max().item()) >= world:
         # (a table entry >= world would drop that bucket's frames on every rank: the
@@ -339,13 +352,14 @@ def gen_shard_index_device(n_global: int, world: int, rank: int, kind: int, n_fl
 
 
 def gen_rss_load_device(n_frames: int, kind: int, n_flows: int, seed: int, counts,
-                        stream: int | None = None) -> None:
-    """Frames per RSS bucket of global frames [0, n_frames) of the synthetic trace
-    into the int64 device tensor `counts` (its length = the table length)."""
-    _lib.check(_lib.lib().tcbee_gen_rss_load_device(
-        C.c_uint64(n_frames), kind, C.c_uint64(n_flows), C.c_uint64(seed),
-        C.c_uint32(int(counts.numel())), _ptr(counts), C.c_void_p(stream or 0)),
-        "tcbee_gen_rss_load_device")
+                        stream: int | None = None, first_frame: int = 0) -> None:
+    """Frames per RSS bucket of global frames [first_frame, first_frame + n_frames)
+    of the synthetic trace into the int64 device tensor `counts` (its length = the
+    table length)."""
+    _lib.check(_lib.lib().tcbee_gen_rss_load_range_device(
+        C.c_uint64(first_frame), C.c_uint64(n_frames), kind, C.c_uint64(n_flows),
+        C.c_uint64(seed), C.c_uint32(int(counts.numel())), _ptr(counts),
+        C.c_void_p(stream or 0)), "tcbee_gen_rss_load_range_device")
 
 
 def gen_shard_scratch_words(n_global: int) -> int:

@@ -30,15 +30,18 @@ class PipeResult:
 class Pipeline:
     def __init__(self, device: int = 0, chunk_frames: int = 1 << 20, window: int = 64,
                  depth: int = 3, threads: int = 8, chunk_bytes: int = 0,
-                 max_flows: int = 1 << 20):
+                 max_flows: int = 1 << 20, variants: bool = False):
+        """variants=True: a pipe of the variants build (TCBEE_PIPE_* A/B settings
+        read from the environment; tests of those paths only)."""
         cfg = _lib.PipeCfg(chunk_frames, chunk_bytes, window, depth, threads, 0)
         h = C.c_void_p()
-        _lib.check(_lib.lib().tcbee_pipe_create(C.byref(h), device, C.byref(cfg), max_flows),
+        self._L = _lib.lib(variants)
+        _lib.check(self._L.tcbee_pipe_create(C.byref(h), device, C.byref(cfg), max_flows),
                    "tcbee_pipe_create")
         self._h = h
         ctx = C.c_void_p()
-        _lib.check(_lib.lib().tcbee_pipe_ctx(h, C.byref(ctx)), "tcbee_pipe_ctx")
-        self.parser = PacketParser._borrow(ctx, device, chunk_frames, max_flows)
+        _lib.check(self._L.tcbee_pipe_ctx(h, C.byref(ctx)), "tcbee_pipe_ctx")
+        self.parser = PacketParser._borrow(ctx, device, chunk_frames, max_flows, self._L)
         self.window = window
 
     def run(self, trace: Trace, filter_port: int = 0, direction: int = _lib.DIR_INGRESS,
@@ -75,7 +78,7 @@ class Pipeline:
         cfg = _lib.Cfg(filter_port, direction, 0, 0 if flows else _lib.F_NO_FLOWS)
         nout = C.c_uint64(0)
         ctr = _lib.Counters()
-        rc = _lib.lib().tcbee_pipe_run(self._h, C.byref(fr), C.byref(cfg), _ptr(rec), cap,
+        rc = self._L.tcbee_pipe_run(self._h, C.byref(fr), C.byref(cfg), _ptr(rec), cap,
                                        _ptr(ids) if flows else 0, cb, None, C.byref(nout),
                                        C.byref(ctr))
         if err:
@@ -93,13 +96,13 @@ class Pipeline:
 
     def stats(self) -> dict:
         st = _lib.PipeStats()
-        _lib.check(_lib.lib().tcbee_pipe_get_stats(self._h, C.byref(st)), "tcbee_pipe_get_stats")
+        _lib.check(self._L.tcbee_pipe_get_stats(self._h, C.byref(st)), "tcbee_pipe_get_stats")
         return {k: int(getattr(st, k)) for k, _ in st._fields_}
 
     def close(self) -> None:
         if self._h:
             self.parser.close()
-            _lib.lib().tcbee_pipe_destroy(self._h)
+            self._L.tcbee_pipe_destroy(self._h)
             self._h = None
 
     def __enter__(self):

@@ -28,8 +28,9 @@ def _ensure_built():
     if not os.path.exists(host_so):
         subprocess.run(["make", "-C", os.path.join(ROOT, "tcbee_amd", "host")], check=True,
                        stdout=subprocess.DEVNULL)
-    lib_so = os.path.join(ROOT, "tcbee_amd", "lib", "libtcbee_amd.so")
-    if not os.path.exists(lib_so):
+    libs = [os.path.join(ROOT, "tcbee_amd", "lib", n)
+            for n in ("libtcbee_amd.so", "libtcbee_amd_variants.so")]
+    if not all(os.path.exists(x) for x in libs):
         subprocess.run(["make", "-C", os.path.join(ROOT, "tcbee_amd", "csrc")], check=True,
                        stdout=subprocess.DEVNULL)
 

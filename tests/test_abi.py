@@ -30,7 +30,7 @@ def test_library_loads_and_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     L = tcbee_amd.lib()
-    assert L.tcbee_abi_version() == 4
+    assert L.tcbee_abi_version() == 5
     assert L.tcbee_strerror(0) == b"ok"
     assert L.tcbee_strerror(_lib.EFLOWFULL) == b"flow table full"
     assert b"first record" in L.tcbee_strerror(_lib.ESHARD)
@@ -152,3 +152,24 @@ def test_exchange_calls_validate_before_device_work():
     assert L.tcbee_status_raise_device(None, p, 2, 4, None) == E
     assert L.tcbee_flow_first_seen_device(None, p, 4, p, None) == E
     assert L.tcbee_flow_first_frames_device(None, p, 4, p, None, p, 4, 4, None) == E
+
+
+def test_variants_library_exports_the_same_abi():
+    """libtcbee_amd_variants.so (test hooks + A/B variants) is the same ABI."""
+    V = _lib.lib(variants=True)
+    for name in header_functions():
+        assert hasattr(V, name), name
+    assert V.tcbee_abi_version() == tcbee_amd.lib().tcbee_abi_version()
+
+
+def test_product_library_reads_no_environment():
+    """the product library carries no TCBEE_* variable name (no
+    getenv of an ablation, A/B variant or test hook: the dispatch is compiled into
+    the variants build only), while the variants build does."""
+    prod = open(_lib.LIB_PATH, "rb").read()
+    var = open(_lib.VARIANTS_LIB_PATH, "rb").read()
+    for name in (b"TCBEE_ABLATE", b"TCBEE_K3ABL", b"TCBEE_K1V", b"TCBEE_TEST_WITHHOLD",
+                 b"TCBEE_TEST_NOPACK", b"TCBEE_NO_FUSE_RANK", b"TCBEE_PIPE_CTHREADS"):
+        assert name in var, name
+    assert re.search(rb"TCBEE_[A-Z0-9_]{2,}", prod) is None
+    assert b"getenv" not in prod

@@ -1,0 +1,73 @@
+"""bench.py's own N>1 path, end to end, on the one-GPU box.
+
+The driver's scaling run launches ``python -m torch.distributed.run ... bench.py
+--gpus N`` over RCCL on N GPUs. RCCL refuses two ranks on one device, so this test
+runs the SAME command at world 2 with the ranks sharing device 0 over gloo
+(TCBEE_DIST_BACKEND=gloo), at reduced frame counts: the config-3 headline as
+flow-hash shards with the held-out RSS table and the FlowHashExchange between K2
+and K3, then the config-4 leg (1M flows of BASELINE.json configs[3], flow-hash
+shards, FlowHashExchange), each ending with every rank's oracle check MIN-reduced
+into ``all_ranks_bit_exact`` (bench.all_ranks_check). The JSON line it prints is
+the one the driver records.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def run_bench_world(world: int, args: list[str], timeout: int = 420) -> dict:
+    env = dict(os.environ, TCBEE_DIST_BACKEND="gloo", PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), "bench.py", "--gpus", str(world)] + args
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=timeout)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints ONE line
+    return json.loads(lines[0])
+
+
+def check_leg(chk: dict, world: int):
+    assert chk["all_ranks_bit_exact"] is True
+    assert chk["ranks_checked"] == world
+    assert chk["global_frames_ok"] and chk["global_pkts_ok"] and chk["global_ingress_ok"]
+    assert chk["shard_imbalance"] < 1.01
+    assert chk["status"] == 0 and chk["sample_bit_exact"]
+
+
+def test_bench_world2_flowhash_and_config4_leg(gpu):
+    out = run_bench_world(2, ["--frames", "4000000", "--steps", "2", "--warmup", "1",
+                              "--c4-frames", "6000000", "--c4-steps", "2"])
+    assert out["n_gpus"] == 2 and out["scaling"] == "weak"
+    assert out["dist"] == {"backend": "gloo", "world_size": 2}
+    assert out["config"]["shard"] == "flowhash" and out["config"]["parallelism"] == "shard2"
+    assert out["value"] > 0 and out["roofline"]["frac"] > 0
+    chk = out["check"]
+    check_leg(chk, 2)
+    assert chk["flows"] == 10_000 and chk["pkts_total"] == 2 * 4_000_000
+    # the RSS table was balanced on frames outside the measured trace
+    assert chk["rss"]["held_out"] is True
+    assert chk["rss"]["balanced_on_frames"][0] == 2 * 4_000_000
+    c4 = out["config4_flowhash"]
+    assert c4["frames_global"] == 12_000_000 and c4["flows"] == 1_000_000
+    assert c4["mpkts"] > 0 and c4["ms_per_step"] > 0
+    check_leg(c4["check"], 2)
+    # 12M IMIX frames of 1M uniform flows: almost every flow appears
+    assert 990_000 < c4["check"]["flows"] <= 1_000_000
+    assert c4["check"]["pkts_total"] == 12_000_000

@@ -62,12 +62,19 @@ def test_gpu_world2_flowhash_shards(gpu, oracle, tmp_path, mode):
     res = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
     owner = fh % world
     if mode != "flowhash":
+        import torch
+
+        import bench
         rss = np.load(tmp_path / "rss0.npy")
         assert np.array_equal(rss, np.load(tmp_path / "rss1.npy"))  # one table on every rank
-        # the table is the LPT balance of the device's bucket loads, which equal the
-        # host partitioner's on the same trace; the host placement agrees frame by frame
-        load = host.flowhash_load(tr, len(rss))
-        assert np.array_equal(rss, tcbee_amd.rss_table(load, world))
+        # the table is the LPT balance of the device's bucket loads over the held-out
+        # window after the trace (bench.rss_for; the device load equals the host
+        # partitioner's: test_rss_load_range_matches_host); the host placement with
+        # that table agrees frame by frame
+        counts = torch.empty(len(rss), dtype=torch.int64, device="cuda")
+        tcbee_amd.gen_rss_load_device(bench.RSS_WINDOW, 1, 3000, tcbee_amd.trace.DEFAULT_SEED,
+                                      counts, first_frame=n)
+        assert np.array_equal(rss, tcbee_amd.rss_table(counts.cpu().numpy(), world))
         owner = rss[fh % len(rss)]
         assert np.array_equal(host.flowhash_owner(tr, world, rss=rss), owner)
         per = np.bincount(owner, minlength=world)
@@ -355,3 +362,54 @@ def test_gpu_replay_pcap_sharded(gpu, oracle, tmp_path, world, filter_port, dire
     assert {k: m[k] for k in ("handled", "dropped", "ingress", "egress")} == ctr
     process_ref.process_records(rec.tobytes(), str(tmp_path / "orc.sqlite"))
     assert process_ref.dump_db(db) == process_ref.dump_db(str(tmp_path / "orc.sqlite"))
+
+
+@pytest.mark.parametrize("first", [0, 120_000, 7_777_777])
+def test_rss_load_range_matches_host(gpu, first):
+    """tcbee_gen_rss_load_range_device over global frames [first, first + m) (the
+    held-out window bench.rss_for balances on) == the host partitioner's bucket
+    loads of the same frames generated on the host."""
+    import torch
+
+    import tcbee_amd
+    from tcbee_amd import host
+    m, nf = 150_000, 3000
+    tr = tcbee_amd.synth_trace(m, sizes="imix", kind=1, n_flows=nf, first_index=first)
+    counts = torch.empty(4096, dtype=torch.int64, device="cuda")
+    tcbee_amd.gen_rss_load_device(m, 1, nf, tcbee_amd.trace.DEFAULT_SEED, counts,
+                                  first_frame=first)
+    assert np.array_equal(counts.cpu().numpy().astype(np.uint64), host.flowhash_load(tr, 4096))
+
+
+def test_rss_table_refused_on_device(gpu):
+    """an RSS table with an entry >= world reaching the C entry point
+    directly (the Python wrapper refuses it earlier) gives the count
+    TCBEE_RSS_INVALID (~0) instead of silently dropping that bucket's frames; the
+    wrapper refuses tables that are not contiguous int16/uint16 device tensors."""
+    import ctypes as C
+
+    import torch
+
+    import tcbee_amd
+    from tcbee_amd import _lib
+    n, world = 50_000, 2
+    scratch = torch.empty(tcbee_amd.gen_shard_scratch_words(n), dtype=torch.int64, device="cuda")
+    n_out = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for bad_at, want_bad in [(None, False), (4095, True), (0, True)]:
+        rss = torch.zeros(4096, dtype=torch.int16, device="cuda")
+        rss[1::2] = 1
+        if bad_at is not None:
+            rss[bad_at] = world
+        _lib.check(_lib.lib().tcbee_gen_shard_index_rss_device(
+            C.c_uint64(n), world, 0, 1, C.c_uint64(500), C.c_uint64(7), 1, rss.data_ptr(),
+            C.c_uint32(4096), None, None, C.c_uint64(0), scratch.data_ptr(), n_out.data_ptr(),
+            None))
+        torch.cuda.synchronize()
+        got = int(n_out.item())
+        assert (got == -1) == want_bad and (want_bad or 0 < got < n)
+    for t in (torch.zeros(64, dtype=torch.int32, device="cuda"),
+              torch.zeros(64, dtype=torch.int16),
+              torch.zeros(128, dtype=torch.int16, device="cuda")[::2]):
+        with pytest.raises(ValueError):
+            tcbee_amd.gen_shard_index_device(n, world, 0, 1, 500, 7, True, None, None, 0,
+                                             scratch, n_out, rss=t)

@@ -233,7 +233,8 @@ def test_tile_shape_determinism(gpu, oracle, fpl, k1v, monkeypatch):
     monkeypatch.setenv("TCBEE_FPL", fpl)
     monkeypatch.setenv("TCBEE_K1V", k1v)
     tr = mixed_trace(150_000, seed=77, n_flows=2000)
-    with tcbee_amd.PacketParser(max_frames=1 << 18, max_arena=1 << 26, max_flows=1 << 14) as p:
+    with tcbee_amd.PacketParser(max_frames=1 << 18, max_arena=1 << 26, max_flows=1 << 14,
+                                variants=True) as p:
         assert_same(p.parse(tr), oracle.parse(tr), p.flows())
 
 
@@ -245,7 +246,8 @@ def test_lookback_recount_fallback(gpu, oracle, every, k1v, monkeypatch):
     monkeypatch.setenv("TCBEE_TEST_WITHHOLD", every)
     monkeypatch.setenv("TCBEE_K1V", k1v)
     tr = mixed_trace(20_000 if every == "1" else 60_000, seed=91, n_flows=300)
-    with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 25, max_flows=1 << 12) as p:
+    with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 25, max_flows=1 << 12,
+                                variants=True) as p:
         assert_same(p.parse(tr), oracle.parse(tr), p.flows())
         assert p.status() == 0
 
@@ -265,7 +267,8 @@ def test_k3_large_table_modes(gpu, oracle, mode, n, flows, monkeypatch):
         monkeypatch.setenv("TCBEE_TEST_K3_NOBUCKET", "1")
     tr = mixed_trace(n, seed=97, n_flows=flows)
     cut = n // 3
-    with tcbee_amd.PacketParser(max_frames=1 << 19, max_arena=1 << 28, max_flows=1 << 18) as p:
+    with tcbee_amd.PacketParser(max_frames=1 << 19, max_arena=1 << 28, max_flows=1 << 18,
+                                variants=mode != "range") as p:
         r1 = p.parse(tr.slice(0, cut))
         r2 = p.parse(tr.slice(cut, n))
         rec, fh, fi, ctr, table = oracle.parse(tr)
@@ -296,7 +299,8 @@ def test_k3_big_caplen_and_hot_flow(gpu, oracle, flows, nopack, monkeypatch):
     # 2^20-1+ leaves the 20-bit caplen of a K3 mode-1 region entry (flows=20000)
     ln[big] = rng.integers(16_000, pad, size=len(big)).astype(np.uint32)
     tr2 = Trace(arena, tr.offset, ln, tr.ts_ns)
-    with tcbee_amd.PacketParser(max_frames=1 << 18, max_arena=1 << 27, max_flows=1 << 16) as p:
+    with tcbee_amd.PacketParser(max_frames=1 << 18, max_arena=1 << 27, max_flows=1 << 16,
+                                variants=nopack == "1") as p:
         assert_same(p.parse(tr2), oracle.parse(tr2), p.flows())
         assert p.status() == 0
 
@@ -643,7 +647,8 @@ def test_k3_chunked_scatter(gpu, oracle, variant, flows, monkeypatch):
     mt = Trace(np.concatenate([mt.arena, np.zeros(pad, np.uint8)]), mt.offset, ln, mt.ts_ns)
     tr = _concat(mt, tcbee_amd.synth_trace(70_000, sizes="64", kind=0, n_flows=1))
     cut = 150_000
-    with tcbee_amd.PacketParser(max_frames=1 << 19, max_arena=1 << 28, max_flows=1 << 18) as p:
+    with tcbee_amd.PacketParser(max_frames=1 << 19, max_arena=1 << 28, max_flows=1 << 18,
+                                variants=True) as p:
         r1 = p.parse(tr.slice(0, cut))
         assert p.count_mode() == 1
         r2 = p.parse(tr.slice(cut, tr.n))
@@ -668,7 +673,8 @@ def test_small_context_fused_rank(gpu, oracle, monkeypatch, fuse):
     tr = mixed_trace(80_000, seed=909, n_flows=60)
     rec, fh, fi, ctr, table = oracle.parse(tr)
     assert 0 < len(table) <= 256
-    with tcbee_amd.PacketParser(max_frames=1 << 20, max_arena=1 << 27, max_flows=256) as p:
+    with tcbee_amd.PacketParser(max_frames=1 << 20, max_arena=1 << 27, max_flows=256,
+                                variants=not fuse) as p:
         ft = oracle.new_flowtab()
         base = 0
         try:
@@ -687,3 +693,66 @@ def test_small_context_fused_rank(gpu, oracle, monkeypatch, fuse):
             p.reset_flows()
             res = p.parse(one)
             assert_same(res, oracle.parse(one), p.flows())
+
+
+@pytest.mark.parametrize("fuse", [True, False])
+def test_small_context_big_frames_over_k3_blocks(gpu, oracle, monkeypatch, fuse):
+    """a small context's fused rank (<= 256 flows) with frames of
+    >= 64 KiB caplen — counted by device atomics, by local id — spread over many K3
+    blocks, in flows that are new in the batch: every block must resolve a new flow's
+    local id itself and its counters must be zero before any block adds (k_prep
+    zeroes the ids not yet handed out); loopback-sized 70 000-B frames, three
+    batches (the second one after a reset), records, ids and table vs the oracle."""
+    monkeypatch.setenv("TCBEE_NO_FUSE_RANK", "0" if fuse else "1")
+    tr = tcbee_amd.synth_trace(400_000, sizes="imix", kind=1, n_flows=200)
+    rng = np.random.default_rng(17)
+    big = rng.choice(tr.n, size=3000, replace=False)
+    pad = 80_000
+    ln = tr.caplen.copy()
+    ln[big] = rng.integers(65_536, 70_001, size=len(big)).astype(np.uint32)
+    tr = Trace(np.concatenate([tr.arena, np.zeros(pad, np.uint8)]), tr.offset, ln, tr.ts_ns)
+    with tcbee_amd.PacketParser(max_frames=1 << 19, max_arena=1 << 28, max_flows=256,
+                                variants=not fuse) as p:
+        for lo, hi, reset in [(0, 250_000, True), (250_000, 400_000, True),
+                              (0, 400_000, False)]:
+            if reset:
+                p.reset_flows()
+            part = tr.slice(lo, hi)
+            if reset:
+                assert_same(p.parse(part), oracle.parse(part), p.flows())
+            else:
+                # the table holds batch 2's flows, the record base its records
+                ft = oracle.new_flowtab()
+                try:
+                    prev = oracle.parse(tr.slice(250_000, 400_000), ft=ft)
+                    orc = oracle.parse(part, ft=ft, record_base=len(prev[0]))
+                    assert_same(p.parse(part), orc)
+                    assert np.array_equal(p.flows(), oracle.flows(ft))
+                finally:
+                    oracle.free_flowtab(ft)
+            assert p.status() == 0
+
+
+def test_product_library_ignores_variant_env(gpu, oracle, monkeypatch):
+    """the product library reads no environment variable. With the
+    ablation / test-hook variables set (ABLATE=8 replaces frame offsets by i*64,
+    K3ABL=1 skips the pkts/bytes bins, NOPACK/WITHHOLD/NO_FUSE_RANK select test
+    paths), a product context still matches the oracle bit-exact, while a context of
+    the variants build does follow them (its records differ) — so the setting took."""
+    from tracegen import mixed_trace
+    for k, v in {"TCBEE_ABLATE": "8", "TCBEE_K3ABL": "1", "TCBEE_TEST_NOPACK": "1",
+                 "TCBEE_TEST_WITHHOLD": "3", "TCBEE_NO_FUSE_RANK": "1", "TCBEE_K1V": "20",
+                 "TCBEE_FPL": "4", "TCBEE_TEST_K3_NORANGE": "1", "TCBEE_STAGE": "1",
+                 "TCBEE_NT": "1", "TCBEE_PROBE_AUX": "16", "TCBEE_WALK": "0"}.items():
+        monkeypatch.setenv(k, v)
+    tr = mixed_trace(120_000, seed=808, n_flows=2000)
+    orc = oracle.parse(tr)
+    with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 26, max_flows=1 << 14) as p:
+        assert_same(p.parse(tr), orc, p.flows())
+        assert p.status() == 0
+    monkeypatch.delenv("TCBEE_K1V")  # (variant 20 takes precedence over the ablation)
+    with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 26, max_flows=1 << 14,
+                                variants=True) as v:
+        res = v.parse(tr)
+        assert res.n == len(orc[0])
+        assert not np.array_equal(res.records, orc[0])

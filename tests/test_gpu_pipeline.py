@@ -38,13 +38,14 @@ def check_same(res, orc, flows_gpu=None):
     (64, 4096, 3, 8), (64, 1000, 4, 1),
 ])
 def test_pipeline_matches_oracle(gpu, oracle, window, chunk, depth, threads, nt, monkeypatch):
-    """TCBEE_PIPE_NT=1 (default): the header-window gather copies whole windows with
-    streaming stores, so the staged bytes past a frame's caplen are the NEXT frame's
-    (mixed_trace's arena is random bytes everywhere); =0: memcpy of caplen bytes."""
+    """The product pipe (TCBEE_PIPE_NT=1 behaviour): the header-window gather copies
+    whole windows with streaming stores, so the staged bytes past a frame's caplen are
+    the NEXT frame's (mixed_trace's arena is random bytes everywhere); the variants
+    build with TCBEE_PIPE_NT=0: memcpy of caplen bytes."""
     monkeypatch.setenv("TCBEE_PIPE_NT", nt)
     t = mixed_trace(60_000, seed=100 + chunk, n_flows=300)
     with Pipeline(device=0, chunk_frames=chunk, window=window, depth=depth,
-                  threads=threads, max_flows=1 << 12) as p:
+                  threads=threads, max_flows=1 << 12, variants=nt == "0") as p:
         res = p.run(t)
         check_same(res, oracle.parse(t), p.flows())
         st = p.stats()
@@ -67,7 +68,7 @@ def test_pipeline_windows_at_arena_end(gpu, oracle, nt, window, monkeypatch):
     t2 = Trace.from_frames(frames)
     assert int(t2.offset[-1] + t2.caplen[-1]) == len(t2.arena)
     with Pipeline(device=0, chunk_frames=1024, window=window, depth=3, threads=4,
-                  max_flows=1 << 12) as p:
+                  max_flows=1 << 12, variants=nt == "0") as p:
         check_same(p.run(t2), oracle.parse(t2), p.flows())
 
 

@@ -1,4 +1,5 @@
 #!/bin/bash
+export TCBEE_AB_LIB=${TCBEE_AB_LIB:-tcbee_amd/lib/libtcbee_amd_variants.so}  # TCBEE_* variants: variants build only
 # Timing-only K1 ablations (TCBEE_ABLATE bits, see k_parse): one process per variant,
 # two interleaved passes.
 for r in 1 2; do for b in 0 1 2 4 8 16 3 31; do

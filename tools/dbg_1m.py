@@ -1,5 +1,7 @@
 """Debug: 1M-flow device parse vs the oracle, mismatch anatomy (round 3)."""
 import os, sys
+# TCBEE_* variants / ablations are dispatched by the variants build only
+os.environ.setdefault("TCBEE_AB_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tcbee_amd", "lib", "libtcbee_amd_variants.so"))
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]

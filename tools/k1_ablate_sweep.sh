@@ -1,4 +1,5 @@
 #!/bin/bash
+export TCBEE_AB_LIB=${TCBEE_AB_LIB:-tcbee_amd/lib/libtcbee_amd_variants.so}  # TCBEE_* variants: variants build only
 # K1 cost breakdown (timing-only ablations, TCBEE_ABLATE bits of k_parse: 1 no
 # look-back, 2 no record stores, 4 no header loads, 8 no index loads, 16 no side
 # outputs): one process per setting (the launcher reads the variable once), same

@@ -1,4 +1,5 @@
 #!/bin/bash
+export TCBEE_AB_LIB=${TCBEE_AB_LIB:-tcbee_amd/lib/libtcbee_amd_variants.so}  # TCBEE_* variants: variants build only
 # K1 variant A/B (TCBEE_K1V), one process, interleaved rounds (tools/k1_sweep.py).
 set -u
 mkdir -p gpurun_out

@@ -1,4 +1,5 @@
 #!/bin/bash
+export TCBEE_AB_LIB=${TCBEE_AB_LIB:-tcbee_amd/lib/libtcbee_amd_variants.so}  # TCBEE_* variants: variants build only
 # K3 mode-1 A/B (round 3): k_count_chunk2 (default, 12288-record chunks, two
 # workgroups per CU; 94 = its 512-thread form) vs round 2's k_count_chunk (93), on
 # the config-4 share's flow count (125k) and the whole 1M-flow trace, 125M frames,

@@ -1,4 +1,5 @@
 #!/bin/bash
+export TCBEE_AB_LIB=${TCBEE_AB_LIB:-tcbee_amd/lib/libtcbee_amd_variants.so}  # TCBEE_* variants: variants build only
 # K3 mode-1 (k_count_scatter) ablations on one GPU's share of config 4
 # (--virtual-world 8: 125M IMIX frames, 125k flows), one rocprofv3 kernel trace
 # per TCBEE_K3ABL variant (timing only; outputs are wrong for variants != 0).
