@@ -477,6 +477,17 @@ int tcbee_pipe_get_stats(const tcbee_pipe* p, tcbee_pipe_stats* st);
 int tcbee_pipe_run(tcbee_pipe* p, const tcbee_frames* in_host, const tcbee_cfg* cfg,
                    uint8_t* out_rec74, uint64_t out_cap, uint32_t* out_flow_id,
                    tcbee_pipe_sink_fn fn, void* user, uint64_t* out_n, tcbee_counters* ctr);
+/* ABI 5. Page-lock the caller's output arrays (hipHostRegister) once, so that
+ * later tcbee_pipe_run calls with these same out_rec74 / out_flow_id (and an
+ * out_cap <= cap) DMA each chunk's records and ids straight into them — no pinned
+ * staging and no host copy-out (the copy-out read + wrote every record again,
+ * ~220 B of host-memory traffic per record). A chunk whose records would pass
+ * out_cap still goes through staging. The sink then receives pointers into the
+ * caller's arrays. out_flow_id may be NULL (records only). Registering another
+ * pair (or NULL, 0, NULL) releases the previous one; tcbee_pipe_destroy releases
+ * it too. The caller keeps the arrays alive while registered. */
+int tcbee_pipe_register_output(tcbee_pipe* p, uint8_t* out_rec74, uint64_t cap,
+                               uint32_t* out_flow_id);
 
 /* ---- host utilities (no GPU needed) ------------------------------------- */
 /* tcbee flow hash v1 of a 40-byte key (DESIGN.md "Flow hash"). */

@@ -194,6 +194,7 @@ _SIGS = {
     "tcbee_pipe_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(PipeCfg),
                                     C.c_uint64]),
     "tcbee_pipe_destroy": (C.c_int, [C.c_void_p]),
+    "tcbee_pipe_register_output": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
     "tcbee_pipe_ctx": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
     "tcbee_pipe_get_stats": (C.c_int, [C.c_void_p, C.POINTER(PipeStats)]),
     "tcbee_pipe_run": (C.c_int, [C.c_void_p, C.POINTER(Frames), C.POINTER(Cfg), C.c_void_p,

@@ -54,6 +54,18 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 
 constexpr uint32_t kSpinLimit = 1u << 24;
 constexpr uint32_t kRecountSpins = 4096;  // ~0.1 ms of polling before recounting
+// K1's wave priority while a tile's index and header loads are issued (then 0).
+// Build-time knob for A/B libraries only (tools/lib_ab.sh, HIPEXTRA=-D...).
+#ifndef TCBEE_K1_LOAD_PRIO
+#define TCBEE_K1_LOAD_PRIO 2
+#endif
+constexpr int kK1LoadPrio = TCBEE_K1_LOAD_PRIO;
+// K3 (mode 0 k_count, mode 1 k_count_chunk2): the same load-phase priority around
+// each iteration's / chunk's record-word loads (0: off)
+#ifndef TCBEE_K3_LOAD_PRIO
+#define TCBEE_K3_LOAD_PRIO 0
+#endif
+constexpr int kK3LoadPrio = TCBEE_K3_LOAD_PRIO;
 [[maybe_unused]] constexpr int kAuxSc1 = 16;  // buffer cache-policy bits: sc1 (agent coherence, bypass L1)
 constexpr int kAuxPlain = 0;  // plain: L1/L2 allocating
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -695,7 +707,7 @@ void k_parse(ParseArgs a) {
   const uint64_t i0 = tile * (uint64_t)TILE;
   // a starting wave issues its index and header loads ahead of resident waves'
   // parse / record work (priority dropped once they are in flight, load_windows)
-  __builtin_amdgcn_s_setprio(2);
+  __builtin_amdgcn_s_setprio(kK1LoadPrio);
   // flows claimed before this batch (claims below it have first records in earlier
   // batches: their frames never compete for first_seen)
   const uint64_t fbase = FLOWS ? a.persist->flow_count : 0;
@@ -1756,7 +1768,9 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   };
   for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
     uint32_t s[U], len[U], id[U];
+    if (kK3LoadPrio) __builtin_amdgcn_s_setprio(kK3LoadPrio);
     load_acc<U, PACK>(c, base + tid, lo, hi, s, len);  // streamed once: non-temporal
+    if (kK3LoadPrio) __builtin_amdgcn_s_setprio(0);
     if (ABL3 & 2) {
 #pragma unroll
       for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : (s[k] & 8191u);
@@ -2073,12 +2087,14 @@ void k_count_chunk2(CountArgs c) {
     // workgroups share a CU)
     const uint32_t* af = c.acc_flow + base;
     const uint32_t* al = c.acc_len + base;
+    if (kK3LoadPrio) __builtin_amdgcn_s_setprio(kK3LoadPrio);
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const uint32_t pos = (uint32_t)k * BS + tid;
       w[k] = __builtin_nontemporal_load(&af[pos < nval ? pos : 0u]);
       if (!PACK) lp[k] = __builtin_nontemporal_load(&al[pos < nval ? pos : 0u]);  // (lp: len)
     }
+    if (kK3LoadPrio) __builtin_amdgcn_s_setprio(0);
     // decode: claim | min(caplen, kLenSat) << 21 (~0: no flow). A caplen of
     // >= kLenSat (2047 B: never on an IMIX trace) is rare: the wave then redoes its
     // words with the full value (the side array when the packed field saturated) and

@@ -163,6 +163,7 @@ struct Slot {
   hipEvent_t ev_h2d = nullptr, ev_parse = nullptr, ev_d2h = nullptr;
   // chunk bookkeeping
   uint64_t lo = 0, hi = 0, arena_used = 0, n_rec = 0, first_record = 0;
+  bool direct = false;  // records / ids were DMA'd into the caller's registered arrays
 };
 
 }  // namespace
@@ -176,6 +177,11 @@ struct tcbee_pipe {
   Pool* pool = nullptr;   // the gather (stage) threads, the main thread included
   Pool* cpool = nullptr;  // the copy-out (consume) threads, the consumer thread included
   tcbee_pipe_stats st{};
+  // caller output arrays registered with tcbee_pipe_register_output (page-locked):
+  // chunks D2H straight into them
+  uint8_t* reg_rec = nullptr;
+  uint32_t* reg_id = nullptr;
+  uint64_t reg_cap = 0;
   uint64_t prefetch = 48;  // header-window gather: frames ahead (TCBEE_PIPE_PF, 0 = off)
   int nt_copy = 1;         // header-window gather: fixed-size 16-B loads + streaming
                            // stores into the staging (TCBEE_PIPE_NT=0: memcpy)
@@ -183,12 +189,21 @@ struct tcbee_pipe {
 
 namespace {
 
+void unregister_output(tcbee_pipe* p) {
+  if (p->reg_rec) (void)hipHostUnregister(p->reg_rec);
+  if (p->reg_id) (void)hipHostUnregister(p->reg_id);
+  p->reg_rec = nullptr;
+  p->reg_id = nullptr;
+  p->reg_cap = 0;
+}
+
 void free_pipe(tcbee_pipe* p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
   if (p->s_h2d) (void)hipStreamSynchronize(p->s_h2d);
   if (p->s_d2h) (void)hipStreamSynchronize(p->s_d2h);
   if (p->ctx) (void)tcbee_ctx_sync(p->ctx);
+  unregister_output(p);
   for (Slot& s : p->slots) {
     for (void* h : {(void*)s.h_arena, (void*)s.h_off, (void*)s.h_len, (void*)s.h_ts,
                     (void*)s.h_rec, (void*)s.h_id, (void*)s.h_meta})
@@ -367,14 +382,22 @@ int enqueue(tcbee_pipe* p, Slot& s, const tcbee_cfg* cfg) {
   return TCBEE_OK;
 }
 
-int fetch(tcbee_pipe* p, Slot& s, bool flows) {
+// D2H of a parsed chunk's records (+ ids): straight into the caller's registered
+// arrays at record `first` when the whole chunk fits below out_cap (s.direct),
+// else into the slot's pinned staging. Chunks are fetched in order, so `first`
+// (records of earlier chunks) is known here.
+int fetch(tcbee_pipe* p, Slot& s, bool flows, uint64_t first, uint8_t* dst_rec, uint32_t* dst_id,
+          uint64_t out_cap) {
   TRY_HIP(hipEventSynchronize(s.ev_parse));
   s.n_rec = s.h_meta[0];
+  s.first_record = first;
+  s.direct = dst_rec && first + s.n_rec <= out_cap && (!flows || dst_id);
   if (s.n_rec) {
-    TRY_HIP(hipMemcpyAsync(s.h_rec, s.d_rec, s.n_rec * TCBEE_RECORD_BYTES, hipMemcpyDeviceToHost,
+    uint8_t* rec = s.direct ? dst_rec + first * TCBEE_RECORD_BYTES : s.h_rec;
+    uint32_t* id = s.direct ? dst_id + first : s.h_id;
+    TRY_HIP(hipMemcpyAsync(rec, s.d_rec, s.n_rec * TCBEE_RECORD_BYTES, hipMemcpyDeviceToHost,
                            p->s_d2h));
-    if (flows)
-      TRY_HIP(hipMemcpyAsync(s.h_id, s.d_id, s.n_rec * 4, hipMemcpyDeviceToHost, p->s_d2h));
+    if (flows) TRY_HIP(hipMemcpyAsync(id, s.d_id, s.n_rec * 4, hipMemcpyDeviceToHost, p->s_d2h));
   }
   TRY_HIP(hipEventRecord(s.ev_d2h, p->s_d2h));
   return TCBEE_OK;
@@ -436,6 +459,27 @@ int tcbee_pipe_create(tcbee_pipe** out, int device, const tcbee_pipe_cfg* pc,
   return TCBEE_OK;
 }
 
+int tcbee_pipe_register_output(tcbee_pipe* p, uint8_t* out_rec74, uint64_t cap,
+                               uint32_t* out_flow_id) {
+  if (!p || (cap && !out_rec74) || (!cap && (out_rec74 || out_flow_id))) return TCBEE_EINVAL;
+  TRY_HIP(hipSetDevice(p->device));
+  TRY_HIP(hipStreamSynchronize(p->s_d2h));  // no D2H into the old arrays in flight
+  unregister_output(p);
+  if (!cap) return TCBEE_OK;
+  TRY_HIP(hipHostRegister(out_rec74, cap * TCBEE_RECORD_BYTES, hipHostRegisterDefault));
+  p->reg_rec = out_rec74;
+  if (out_flow_id) {
+    const hipError_t e = hipHostRegister(out_flow_id, cap * 4, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+      unregister_output(p);
+      return map_err(e);
+    }
+    p->reg_id = out_flow_id;
+  }
+  p->reg_cap = cap;
+  return TCBEE_OK;
+}
+
 int tcbee_pipe_destroy(tcbee_pipe* p) {
   if (!p) return TCBEE_EINVAL;
   free_pipe(p);
@@ -466,7 +510,12 @@ int tcbee_pipe_run(tcbee_pipe* p, const tcbee_frames* in, const tcbee_cfg* cfg,
   TRY_HIP(hipSetDevice(p->device));
   const bool flows = !(cfg->flags & TCBEE_F_NO_FLOWS);
   const uint64_t D = p->slots.size();
-  uint64_t written = 0, records = 0, chunks = 0;
+  // the caller's arrays are the registered ones: chunks D2H straight into them
+  const bool reg = p->reg_rec && out_rec74 == p->reg_rec && out_cap <= p->reg_cap &&
+                   (!flows || !out_flow_id || out_flow_id == p->reg_id);
+  uint8_t* const dst_rec = reg ? out_rec74 : nullptr;
+  uint32_t* const dst_id = reg && flows ? out_flow_id : nullptr;
+  uint64_t written = 0, records = 0, chunks = 0, fetched_records = 0;
   tcbee_counters sum{};
   int rc = TCBEE_OK;
 
@@ -480,8 +529,11 @@ int tcbee_pipe_run(tcbee_pipe* p, const tcbee_frames* in, const tcbee_cfg* cfg,
     sum.handled += s.h_meta[3];
     sum.dropped += s.h_meta[4];
     const uint64_t n = s.n_rec;
-    s.first_record = records;
-    if (out_rec74 && records < out_cap) {
+    const uint8_t* rec = s.direct ? out_rec74 + records * TCBEE_RECORD_BYTES : s.h_rec;
+    const uint32_t* ids = s.direct ? (out_flow_id ? out_flow_id + records : nullptr) : s.h_id;
+    if (s.direct) {
+      written += n;  // already in place
+    } else if (out_rec74 && records < out_cap) {
       const uint64_t k = n < out_cap - records ? n : out_cap - records;
       uint8_t* dst = out_rec74 + records * TCBEE_RECORD_BYTES;
       uint32_t* did = out_flow_id ? out_flow_id + records : nullptr;
@@ -495,7 +547,7 @@ int tcbee_pipe_run(tcbee_pipe* p, const tcbee_frames* in, const tcbee_cfg* cfg,
     }
     records += n;
     if (fn) {
-      int urc = fn(user, s.h_rec, flows ? s.h_id : nullptr, n, s.first_record);
+      int urc = fn(user, rec, flows ? ids : nullptr, n, s.first_record);
       if (urc) return urc;
     }
     return TCBEE_OK;
@@ -550,12 +602,16 @@ int tcbee_pipe_run(tcbee_pipe* p, const tcbee_frames* in, const tcbee_cfg* cfg,
     ++issued;
     ++chunks;
     if (fetched + 1 < issued) {
-      if ((rc = fetch(p, p->slots[fetched % D], flows))) break;
+      Slot& f = p->slots[fetched % D];
+      if ((rc = fetch(p, f, flows, fetched_records, dst_rec, dst_id, out_cap))) break;
+      fetched_records += f.n_rec;
       hand_over(fetched++);
     }
   }
   while (rc == TCBEE_OK && fetched < issued) {
-    if ((rc = fetch(p, p->slots[fetched % D], flows))) break;
+    Slot& f = p->slots[fetched % D];
+    if ((rc = fetch(p, f, flows, fetched_records, dst_rec, dst_id, out_cap))) break;
+    fetched_records += f.n_rec;
     hand_over(fetched++);
   }
   {

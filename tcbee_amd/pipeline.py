@@ -43,6 +43,28 @@ class Pipeline:
         _lib.check(self._L.tcbee_pipe_ctx(h, C.byref(ctx)), "tcbee_pipe_ctx")
         self.parser = PacketParser._borrow(ctx, device, chunk_frames, max_flows, self._L)
         self.window = window
+        self._registered = None  # (out_rec, out_id) page-locked for direct D2H
+
+    def register_output(self, out_rec, out_id=None) -> None:
+        """Page-lock the caller's output arrays once (tcbee_pipe_register_output):
+        later run(..., out_rec=out_rec, out_id=out_id) calls DMA each chunk's records
+        and ids straight into them instead of staging + a host copy-out. The arrays
+        are kept referenced while registered; register_output(None) releases them."""
+        if out_rec is None:
+            _lib.check(self._L.tcbee_pipe_register_output(self._h, None, 0, None),
+                       "tcbee_pipe_register_output")
+            self._registered = None
+            return
+        if (out_rec.dtype != np.uint8 or out_rec.ndim != 2 or out_rec.shape[1] != _lib.RECORD_BYTES
+                or not out_rec.flags.c_contiguous):
+            raise ValueError("out_rec: a C-contiguous uint8 [n, 74] array")
+        if out_id is not None and (out_id.dtype != np.uint32 or not out_id.flags.c_contiguous
+                                   or len(out_id) < len(out_rec)):
+            raise ValueError("out_id: a C-contiguous uint32 array of at least len(out_rec)")
+        _lib.check(self._L.tcbee_pipe_register_output(self._h, _ptr(out_rec), len(out_rec),
+                                                      _ptr(out_id)),
+                   "tcbee_pipe_register_output")
+        self._registered = (out_rec, out_id)
 
     def run(self, trace: Trace, filter_port: int = 0, direction: int = _lib.DIR_INGRESS,
             flows: bool = True, collect: bool = True, sink=None, out_rec=None,
@@ -102,8 +124,9 @@ class Pipeline:
     def close(self) -> None:
         if self._h:
             self.parser.close()
-            self._L.tcbee_pipe_destroy(self._h)
+            self._L.tcbee_pipe_destroy(self._h)  # (releases a registered output too)
             self._h = None
+            self._registered = None
 
     def __enter__(self):
         return self

@@ -128,6 +128,51 @@ def test_pipeline_sink_callback_and_out_cap(gpu, oracle):
         assert np.array_equal(small, rec[:100])
 
 
+@pytest.mark.parametrize("window", [64, 0])
+def test_pipeline_registered_output(gpu, oracle, window):
+    """the caller's arrays registered once (tcbee_pipe_register_output):
+    chunks DMA straight into them. Records / ids / counters equal the oracle; the
+    sink sees the same records (pointers into the caller's arrays); flow ids continue
+    across runs; a registered array with a smaller out_cap than the records sends the
+    chunk past it through staging (ECAPACITY, the first out_cap written); ids not
+    registered (records only) and unregistering fall back to staging, same bytes."""
+    t = mixed_trace(50_000, seed=61, n_flows=400)
+    rec, fh, fi, ctr, table = oracle.parse(t)
+    n = len(rec)
+    out = np.zeros((n + 50, 74), np.uint8)
+    ids = np.zeros(n + 50, np.uint32)
+    with Pipeline(device=0, chunk_frames=4096, window=window, depth=3, threads=4,
+                  max_flows=1 << 12) as p:
+        p.register_output(out, ids)
+        seen = []
+        res = p.run(t, out_rec=out, out_id=ids,
+                    sink=lambda r, i, first: seen.append((first, r.copy(), i.copy())))
+        check_same(res, (rec, fh, fi, ctr, table), p.flows())
+        assert not out[n:].any() and not ids[n:].any()
+        assert np.array_equal(np.concatenate([r for _, r, _ in seen]), rec)
+        assert np.array_equal(np.concatenate([i for _, _, i in seen]), fi)
+        # a second run continues the ids; reset: the same bytes again
+        p.reset_flows()
+        out[:] = 0
+        check_same(p.run(t, out_rec=out, out_id=ids), (rec, fh, fi, ctr, table))
+        # out_cap below the records: the overflowing chunk goes through staging
+        p.reset_flows()
+        out[:] = 0
+        with pytest.raises(tcbee_amd.TcbeeError) as e:
+            p.run(t, out_rec=out[:n - 5000], out_id=ids)
+        assert e.value.code == tcbee_amd._lib.ECAPACITY
+        assert np.array_equal(out[:n - 5000], rec[:n - 5000]) and not out[n - 5000:].any()
+        # records-only registration, then none at all: staging, identical results
+        for reg in ((out, None), (None, None)):
+            p.register_output(*reg)
+            p.reset_flows()
+            out[:] = 0
+            ids[:] = 0
+            check_same(p.run(t, out_rec=out[:n], out_id=ids[:n]), (rec, fh, fi, ctr, table))
+        with pytest.raises(ValueError):
+            p.register_output(np.zeros((10, 70), np.uint8))
+
+
 def test_pipeline_empty_and_tiny(gpu, oracle):
     with Pipeline(device=0, chunk_frames=1024) as p:
         t0 = mixed_trace(0, seed=1)

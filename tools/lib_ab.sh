@@ -18,7 +18,8 @@ case "${1:-}" in
     done
     case $rev in wt:*) cp include/tcbee_amd.h "$d/include/tcbee_amd.h" ;;
                  *) git show "$rev:include/tcbee_amd.h" > "$d/include/tcbee_amd.h" ;; esac
-    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -shared \
+    # HIPEXTRA: extra compiler flags for this build (e.g. -DTCBEE_K1_LOAD_PRIO=3)
+    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function ${HIPEXTRA:-} -shared \
       -o "$d/libtcbee_amd.so" "$d/tcbee_amd/csrc/tcbee_kernels.hip" "$d/tcbee_amd/csrc/tcbee_capi.hip" "$d/tcbee_amd/csrc/tcbee_pipe.hip"
     echo "$d/libtcbee_amd.so" ;;
   run)
