@@ -38,7 +38,8 @@
 extern "C" {
 #endif
 
-#define TCBEE_ABI_VERSION 5  /* 5: tcbee_gen_rss_load_range_device, TCBEE_RSS_INVALID;
+#define TCBEE_ABI_VERSION 5  /* 5: tcbee_gen_rss_load_range_device, TCBEE_RSS_INVALID,
+                                tcbee_ctx_create_ex, tcbee_pipe_register_output;
                               3: owner meta world+2 words, tcbee_status_raise_device;
                                 4: RSS indirection tables for the shard generator */
 
@@ -132,13 +133,26 @@ int         tcbee_device_count(int* n);
 /* ---- context --------------------------------------------------------------
  * max_frames: largest batch (frames) any parse call on this ctx will pass.
  * max_arena : largest arena (bytes) the HOST entry point will copy.
- * max_flows : flow-table capacity in distinct flows (table has >= 2x slots,
- *             a power of two, 64 B each); at most 2^24 (TCBEE_ECAPACITY above:
- *             the table's 2 GiB bound). The table still accepts flows past
- *             max_flows, up to its slot count (TCBEE_EFLOWFULL then).
+ * max_flows : flow-table capacity in distinct flows, an exact bound: the claim
+ *             of a flow past it is refused (TCBEE_EFLOWFULL; its frames stay
+ *             unclassified, flow id ~0); at most 2^24 (TCBEE_ECAPACITY above).
+ *             Device footprint per max_flow: ~171 B of compact
+ *             slots (IPv4-form keys, 8 slots per flow, 3 per 64-B unit) + 104 B of
+ *             per-claim state (key 64, first_seen 8, counters 16, id map 4, new-flow
+ *             list 8, first-seen copy 4) — 275 MB at 1M flows — PLUS the wide slots
+ *             of non-IPv4-form (IPv6) keys: a power of two >= 8 x max_wide_flows
+ *             slots of 64 B (512-1024 B per wide flow: 512 MiB at 1M), allocated
+ *             whatever the trace holds; tcbee_ctx_create sizes them for
+ *             max_wide_flows = max_flows.
  * device    : HIP device ordinal. */
 int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames,
                      uint64_t max_arena, uint64_t max_flows);
+/* ABI 5. The same with the wide slots sized for max_wide_flows (16..max_flows)
+ * non-IPv4-form keys — an exact bound like max_flows: a wide key past it is
+ * refused (TCBEE_EFLOWFULL) without taking a claim. An IPv4-only capture of 1M
+ * flows needs max_wide_flows = 16 (4 KiB of wide slots instead of 512 MiB). */
+int tcbee_ctx_create_ex(tcbee_ctx** out, int device, uint64_t max_frames,
+                        uint64_t max_arena, uint64_t max_flows, uint64_t max_wide_flows);
 int tcbee_ctx_destroy(tcbee_ctx* ctx);
 /* The context's own HIP stream (hipStream_t as void*). */
 int tcbee_ctx_stream(tcbee_ctx* ctx, void** stream);

@@ -108,6 +108,8 @@ _SIGS = {
     "tcbee_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "tcbee_ctx_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_uint64,
                                    C.c_uint64, C.c_uint64]),
+    "tcbee_ctx_create_ex": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_uint64,
+                                      C.c_uint64, C.c_uint64, C.c_uint64]),
     "tcbee_ctx_destroy": (C.c_int, [C.c_void_p]),
     "tcbee_ctx_stream": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
     "tcbee_ctx_sync": (C.c_int, [C.c_void_p]),

@@ -240,6 +240,11 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
 
 int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t max_arena,
                      uint64_t max_flows) {
+  return tcbee_ctx_create_ex(out, device, max_frames, max_arena, max_flows, max_flows);
+}
+
+int tcbee_ctx_create_ex(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t max_arena,
+                        uint64_t max_flows, uint64_t max_wide_flows) {
   if (!out || max_frames == 0) return TCBEE_EINVAL;
   // batch-local record / frame indices are 31-bit (the flow table's fs32 words)
   if (max_frames >= (1ull << 31)) return TCBEE_ECAPACITY;
@@ -284,6 +289,9 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   c->nlines = (kSlotsPerFlow * c->max_flows + kSlotsPerLine - 1) / kSlotsPerLine;
   c->tab.nlines = c->nlines;
   c->tab.max_claims = c->max_flows;
+  // wide-slot (non-IPv4-form: IPv6) keys: at most max_wide_flows of them (16..max_flows)
+  c->tab.max_wide = max_wide_flows < 16 ? 16 : (max_wide_flows < c->max_flows ? max_wide_flows
+                                                                                : c->max_flows);
   {
     // claims < max_flows: ceil(log2(max_flows)) bits + 1 (so no packed word is all
     // ones, the no-flow mark); packed while at least 11 bits remain (a standard
@@ -304,10 +312,10 @@ int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames, uint64_t 
   if ((e = dalloc(&c->tab.ent, 8 * c->max_flows)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.cfs, c->max_flows)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_new_fs, c->max_flows)) != hipSuccess) return fail(map_err(e));
-  // wide slots (non-IPv4-form keys): a power of two >= kSlotsPerFlow x max_flows,
-  // at most 2^25 (2 GiB: K1's probe buffer resource and u32 offsets)
+  // wide slots (non-IPv4-form keys): a power of two >= kSlotsPerFlow x max_wide,
+  // at most 2^25 (2 GiB: K1's probe buffer resource and u32 offsets); 64 B each
   c->tab.wide_mask = 63;
-  while (c->tab.wide_mask + 1 < kSlotsPerFlow * c->max_flows && c->tab.wide_mask + 1 < (1ull << 25))
+  while (c->tab.wide_mask + 1 < kSlotsPerFlow * c->tab.max_wide && c->tab.wide_mask + 1 < (1ull << 25))
     c->tab.wide_mask = 2 * c->tab.wide_mask + 1;
   if ((e = dalloc(&c->tab.wide, 8 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
   // all ones, then every tag word zero (k_table_init sweeps the wide slots only once

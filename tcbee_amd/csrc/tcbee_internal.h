@@ -61,6 +61,8 @@ struct FlowTable {
   uint32_t* cmap;        // claim index -> dense id (0-based), written by K2; dense in
                          // [0, flows), so K3 stages it in LDS
   uint64_t max_claims;   // claims at or past it are refused (TCBEE_EFLOWFULL)
+  uint64_t max_wide;     // claims of wide-slot (non-IPv4-form) keys past it are refused
+                         // too (tcbee_ctx_create_ex; = max_claims by default)
 };
 constexpr uint32_t kSlotsPerLine = 3;  // compact slots per 64-B unit
 constexpr uint32_t kWideSlot = 1u << 31;  // slot ids: compact s, or wide s | kWideSlot
@@ -78,6 +80,7 @@ struct PersistState {
   // k_assign reads the old bases without any grid-wide completion count
   uint64_t rank_base;
   uint64_t rank_fbase;
+  uint64_t wide_claims;  // wide-slot keys claimed (bounded by FlowTable::max_wide)
 };
 
 // Zeroed before every batch (one 32-B memset).

@@ -460,10 +460,17 @@ __device__ uint32_t flow_upsert_wide(const FlowTable& T, const uint64_t (&K)[5],
       if (__hip_atomic_compare_exchange_strong(m, &expected, kTagBusy, __ATOMIC_RELAXED,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         if (!ld_agent32(T.wide_used)) st_agent32(T.wide_used, 1u);
-        const uint64_t slot_no = atomicAdd((unsigned long long*)&batch->n_new, 1ull);
-        const uint64_t cl = fbase + slot_no;
 #pragma unroll
         for (int j = 0; j < 5; ++j) st_agent(m + 1 + j, K[j]);
+        // a context with fewer wide slots than max_flows (tcbee_ctx_create_ex) bounds
+        // its wide keys exactly: refused BEFORE a claim number is taken (claims stay
+        // dense), the slot published dead
+        const bool wide_full =
+            T.max_wide < T.max_claims &&
+            atomicAdd((unsigned long long*)&persist->wide_claims, 1ull) >= T.max_wide;
+        const uint64_t slot_no =
+            wide_full ? 0ull : atomicAdd((unsigned long long*)&batch->n_new, 1ull);
+        const uint64_t cl = wide_full ? T.max_claims : fbase + slot_no;
         if (cl >= T.max_claims) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           st_agent(m, (uint64_t)tag | (0xFFFFFFFFull << 32));  // dead

@@ -52,17 +52,21 @@ def _ptr(x) -> int:
 
 class PacketParser:
     def __init__(self, device: int = 0, max_frames: int = 1 << 20, max_arena: int = 0,
-                 max_flows: int = 1 << 16, variants: bool = False):
+                 max_flows: int = 1 << 16, variants: bool = False,
+                 max_wide_flows: int | None = None):
         """variants=True: a context of the variants build (libtcbee_amd_variants.so),
         whose test hooks / A/B variants follow TCBEE_* environment variables read at
         creation — for tests of those alternative paths; the product library ignores
-        the environment."""
+        the environment. max_wide_flows: the bound on non-IPv4-form (IPv6) keys that
+        sizes the 64-B wide slots (tcbee_ctx_create_ex; None = max_flows)."""
         L = _lib.lib(variants)
         self._L = L
         h = C.c_void_p()
-        _lib.check(L.tcbee_ctx_create(C.byref(h), device, C.c_uint64(max_frames),
-                                      C.c_uint64(max_arena), C.c_uint64(max_flows)),
-                   "tcbee_ctx_create")
+        wide = max_flows if max_wide_flows is None else max_wide_flows
+        _lib.check(L.tcbee_ctx_create_ex(C.byref(h), device, C.c_uint64(max_frames),
+                                         C.c_uint64(max_arena), C.c_uint64(max_flows),
+                                         C.c_uint64(wide)),
+                   "tcbee_ctx_create_ex")
         self._h = h
         self._owned = True
         self.device = device

@@ -756,3 +756,37 @@ def test_product_library_ignores_variant_env(gpu, oracle, monkeypatch):
         res = v.parse(tr)
         assert res.n == len(orc[0])
         assert not np.array_equal(res.records, orc[0])
+
+
+@pytest.mark.parametrize("short", [0, 9])
+def test_max_wide_flows_exact_bound(gpu, oracle, short):
+    """tcbee_ctx_create_ex sizes the 64-B wide slots for
+    max_wide_flows non-IPv4-form keys instead of max_flows. With max_wide_flows = the
+    trace's IPv6 keys the context is bit-exact; `short` fewer refuse exactly that many
+    IPv6 keys (TCBEE_EFLOWFULL, frames unclassified, no claim taken: every IPv4 key
+    and the other IPv6 keys keep dense ids), records unchanged."""
+    from tracegen import mixed_trace
+    tr = mixed_trace(60_000, seed=78, n_flows=2500)
+    rec, fh, fi, ctr, table = oracle.parse(tr)
+    t = table["tuple"]
+    wide = (t[:, 0:12].any(axis=1)) | (t[:, 16:28].any(axis=1))
+    nwide = int(wide.sum())
+    assert nwide > 100 and (~wide).sum() > 100
+    with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 25, max_flows=len(table),
+                                max_wide_flows=nwide - short) as p:
+        res = p.parse(tr)
+        assert np.array_equal(res.records, rec)
+        fl = p.flows()
+        if short == 0:
+            assert p.status() == 0
+            assert_same(res, (rec, fh, fi, ctr, table), fl)
+            return
+        assert p.status() == tcbee_amd._lib.EFLOWFULL
+        assert len(fl) == len(table) - short
+        ft = fl["tuple"]
+        assert int(((ft[:, 0:12].any(axis=1)) | (ft[:, 16:28].any(axis=1))).sum()) == nwide - short
+        refused = res.flow_id == 0xFFFFFFFF
+        keys = np.unique(fi[refused])
+        assert len(keys) == short and wide[keys].all()
+        assert res.flow_id[~refused].max() < len(table) - short
+        assert not np.isin(fi[~refused], keys).any()
