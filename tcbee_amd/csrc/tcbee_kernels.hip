@@ -3039,8 +3039,9 @@ hipError_t launch_table_init(FlowTable t, hipStream_t s) {
 #if TCBEE_VARIANTS
 // k1v (TCBEE_K1V at context creation) and the TCBEE_PROBE_AUX / TCBEE_ABLATE /
 // TCBEE_STAGE / TCBEE_NT environment: staging, occupancy, cache-policy A/B variants
-// and timing-only ablations (several write wrong records on purpose). Returns true
-// when it launched a variant.
+// and timing-only ablations (several write wrong records on purpose), read at every
+// launch (a process may switch them between contexts). Returns true when it
+// launched a variant.
 template <int FPL>
 static bool launch_parse_variant(const ParseArgs& a, bool flows, hipStream_t s, int k1v, dim3 grid) {
   if constexpr (FPL == 2) if (flows && k1v) {
@@ -3059,11 +3060,11 @@ static bool launch_parse_variant(const ParseArgs& a, bool flows, hipStream_t s, 
       default: return false;
     }
   }
-  static const int aux = [] {
+  const int aux = [] {
     const char* e = getenv("TCBEE_PROBE_AUX");
     return e ? atoi(e) : kAuxPlain;
   }();
-  static const int abl = [] {
+  const int abl = [] {
     const char* e = getenv("TCBEE_ABLATE");
     return e ? atoi(e) : 0;
   }();
@@ -3080,7 +3081,7 @@ static bool launch_parse_variant(const ParseArgs& a, bool flows, hipStream_t s, 
     }
 #undef TCBEE_ABL_CASE
   }
-  static const int stage = [] {
+  const int stage = [] {
     const char* e = getenv("TCBEE_STAGE");
     return e ? atoi(e) : 0;
   }();
@@ -3089,7 +3090,7 @@ static bool launch_parse_variant(const ParseArgs& a, bool flows, hipStream_t s, 
     else hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain, 0, 1>), grid, dim3(kBlock), 0, s, a);
     return true;
   }
-  static const int nt = [] {
+  const int nt = [] {
     const char* e = getenv("TCBEE_NT");
     return e ? atoi(e) : 0;
   }();

@@ -750,7 +750,9 @@ def test_product_library_ignores_variant_env(gpu, oracle, monkeypatch):
     with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 26, max_flows=1 << 14) as p:
         assert_same(p.parse(tr), orc, p.flows())
         assert p.status() == 0
-    monkeypatch.delenv("TCBEE_K1V")  # (variant 20 takes precedence over the ablation)
+    # (the ablation is dispatched for the default tiling only: FPL 2, no K1 variant)
+    monkeypatch.delenv("TCBEE_K1V")
+    monkeypatch.delenv("TCBEE_FPL")
     with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 26, max_flows=1 << 14,
                                 variants=True) as v:
         res = v.parse(tr)
