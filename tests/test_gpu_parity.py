@@ -756,8 +756,8 @@ def test_product_library_ignores_variant_env(gpu, oracle, monkeypatch):
     with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 26, max_flows=1 << 14,
                                 variants=True) as v:
         res = v.parse(tr)
-        assert res.n == len(orc[0])
-        assert not np.array_equal(res.records, orc[0])
+        # (frames read at i * 64 instead of their offsets: other frames accepted)
+        assert res.n != len(orc[0]) or not np.array_equal(res.records, orc[0])
 
 
 @pytest.mark.parametrize("short", [0, 9])

@@ -1,0 +1,23 @@
+#!/bin/bash
+# K3 mode 1 (k_count_chunk2 + k_count_bucket) on the whole 1M-flow trace
+# (--config4 --shard contig: 125M IMIX frames, 1M flows): what bounds it. Separate
+# --pmc passes (at most 8 SQ_ / 4 TCC_ counters each), each its own short run
+# under a hard limit (MI355X_MICROARCH.md: counters in their own runs).
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+args=(--steps 2 --warmup 1 --no-cpu --no-extra --sample-check ${K3ARGS:---config4 --shard contig})
+pass() {  # name counters...
+  local name=$1; shift
+  timeout -s KILL 300 rocprofv3 --pmc "$@" --output-format csv -d "gpurun_out/$name" -o run \
+    -- python bench.py "${args[@]}" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" >&2
+  [ $rc -eq 0 ] || exit $rc
+}
+pass k3pmc_sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
+  SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS
+pass k3pmc_lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_WAVES \
+  TCC_HIT_sum TCC_MISS_sum
+pass k3pmc_fetch FETCH_SIZE
+pass k3pmc_write WRITE_SIZE
