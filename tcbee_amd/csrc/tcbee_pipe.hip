@@ -96,20 +96,23 @@ class Pool {
     for (auto& t : th_) t.join();
   }
   unsigned size() const { return n_; }
-  // fn(part, parts) on every thread (the caller is part 0); returns when all are done.
-  void run(const std::function<void(unsigned, unsigned)>& fn) {
-    if (n_ == 1) {
+  // fn(part, parts) on the first `parts` threads (all by default; the caller is part
+  // 0); returns when all are done.
+  void run(const std::function<void(unsigned, unsigned)>& fn, unsigned parts = 0) {
+    parts = parts == 0 || parts > n_ ? n_ : parts;
+    if (parts == 1) {
       fn(0, 1);
       return;
     }
     {
       std::lock_guard<std::mutex> g(m_);
       fn_ = &fn;
+      parts_ = parts;
       pending_ = n_ - 1;
       ++gen_;
     }
     cv_.notify_all();
-    fn(0, n_);
+    fn(0, parts);
     std::unique_lock<std::mutex> lk(m_);
     done_cv_.wait(lk, [this] { return pending_ == 0; });
     fn_ = nullptr;
@@ -120,14 +123,16 @@ class Pool {
     uint64_t seen = 0;
     for (;;) {
       const std::function<void(unsigned, unsigned)>* fn;
+      unsigned parts;
       {
         std::unique_lock<std::mutex> lk(m_);
         cv_.wait(lk, [&] { return gen_ != seen; });
         seen = gen_;
         if (stop_) return;
         fn = fn_;
+        parts = parts_;
       }
-      (*fn)(id, n_);
+      if (id < parts) (*fn)(id, parts);
       {
         std::lock_guard<std::mutex> g(m_);
         if (--pending_ == 0) done_cv_.notify_one();
@@ -138,7 +143,7 @@ class Pool {
   std::mutex m_;
   std::condition_variable cv_, done_cv_;
   const std::function<void(unsigned, unsigned)>* fn_ = nullptr;
-  unsigned n_ = 1, pending_ = 0;
+  unsigned n_ = 1, parts_ = 1, pending_ = 0;
   uint64_t gen_ = 0;
   bool stop_ = false;
 };
@@ -176,6 +181,7 @@ struct tcbee_pipe {
   std::vector<Slot> slots;
   Pool* pool = nullptr;   // the gather (stage) threads, the main thread included
   Pool* cpool = nullptr;  // the copy-out (consume) threads, the consumer thread included
+  unsigned gt_staged = 1;  // gather threads while the copy-out pool works (staged outputs)
   tcbee_pipe_stats st{};
   // caller output arrays registered with tcbee_pipe_register_output (page-locked):
   // chunks D2H straight into them
@@ -267,8 +273,9 @@ uint64_t chunk_end(const tcbee_pipe* p, const tcbee_frames* in, uint64_t lo) {
   return i;
 }
 
-// Gather frames [s.lo, s.hi) into the slot's pinned staging (pool-parallel).
-void stage(tcbee_pipe* p, const tcbee_frames* in, Slot& s) {
+// Gather frames [s.lo, s.hi) into the slot's pinned staging on `gparts` of the
+// gather pool's threads (pool-parallel).
+void stage(tcbee_pipe* p, const tcbee_frames* in, Slot& s, unsigned gparts) {
   const uint64_t lo = s.lo, n = s.hi - s.lo, W = p->cfg.window;
   if (W) {
     const uint64_t pf = p->prefetch;
@@ -319,19 +326,19 @@ void stage(tcbee_pipe* p, const tcbee_frames* in, Slot& s) {
 #if TCBEE_PIPE_HAVE_NT
       if (nt) _mm_sfence();  // streaming stores visible before the H2D copy is issued
 #endif
-    });
+    }, gparts);
     s.arena_used = window_base(W) + n * W;
     return;
   }
   // whole frames: exclusive prefix of caplen per part, then copy
-  const unsigned parts = p->pool->size();
+  const unsigned parts = gparts ? gparts : p->pool->size();
   std::vector<uint64_t> part_bytes(parts + 1, 0);
   p->pool->run([&](unsigned part, unsigned np) {
     const uint64_t a = n * part / np, b = n * (part + 1) / np;
     uint64_t sum = 0;
     for (uint64_t k = a; k < b; ++k) sum += in->caplen[lo + k];
     part_bytes[part + 1] = sum;
-  });
+  }, parts);
   for (unsigned i = 0; i < parts; ++i) part_bytes[i + 1] += part_bytes[i];
   p->pool->run([&](unsigned part, unsigned np) {
     const uint64_t a = n * part / np, b = n * (part + 1) / np;
@@ -350,7 +357,7 @@ void stage(tcbee_pipe* p, const tcbee_frames* in, Slot& s) {
       s.h_ts[k] = in->ts_ns[f];
       pos += len;
     }
-  });
+  }, parts);
   s.arena_used = part_bytes[parts];
 }
 
@@ -440,15 +447,16 @@ int tcbee_pipe_create(tcbee_pipe** out, int device, const tcbee_pipe_cfg* pc,
     return free_pipe(p), TCBEE_EDEVICE;
   try {
     p->slots.resize(c.depth);
-    // `threads` in all: a quarter copy records out while the rest gather
-    // (TCBEE_PIPE_CTHREADS: the copy-out share, A/B)
+    // `threads` in all: with staged outputs a quarter copy records out while the
+    // rest gather (TCBEE_PIPE_CTHREADS: the copy-out share, A/B); with the caller's
+    // arrays registered (direct D2H, nothing to copy out) all of them gather
     unsigned ct = c.threads >= 4 ? c.threads / 4 : 1;
 #if TCBEE_VARIANTS
     if (const char* e = std::getenv("TCBEE_PIPE_CTHREADS")) ct = (unsigned)std::atoi(e);
 #endif
     if (ct < 1) ct = 1;
-    const unsigned gt = c.threads > ct ? c.threads - ct : 1;
-    p->pool = new Pool(gt);
+    p->gt_staged = c.threads > ct ? c.threads - ct : 1;
+    p->pool = new Pool(c.threads > p->gt_staged ? c.threads : p->gt_staged);
     p->cpool = new Pool(ct);
   } catch (...) {
     return free_pipe(p), TCBEE_ENOMEM;
@@ -596,7 +604,7 @@ int tcbee_pipe_run(tcbee_pipe* p, const tcbee_frames* in, const tcbee_cfg* cfg,
     Slot& s = p->slots[issued % D];
     s.lo = lo;
     s.hi = chunk_end(p, in, lo);
-    stage(p, in, s);
+    stage(p, in, s, reg ? 0u : p->gt_staged);
     if ((rc = enqueue(p, s, cfg))) break;
     lo = s.hi;
     ++issued;
