@@ -1427,6 +1427,43 @@ __device__ __forceinline__ void load_acc(const CountArgs& c, uint64_t p0, uint64
   }
 }
 
+// The same for packed words, four consecutive records per 16-B load: entry 4k + j
+// is record p0 + 4 k kCountBlock + j (p0 = base + 4 tid, 16-B aligned: block ranges
+// start at multiples of kK3Gran). Four times the bytes in flight per load
+// instruction of the scalar form (K3 mode 0 holds one 1024-thread block per CU).
+template <int U>
+__device__ __forceinline__ void load_acc4(const CountArgs& c, uint64_t p0, uint64_t hi,
+                                          uint32_t (&claim)[4 * U], uint32_t (&len)[4 * U]) {
+  uint32_t v[4 * U];
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    const uint64_t p = p0 + 4ull * k * kCountBlock;
+    if (p + 3 < hi) {
+      const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(c.acc_flow + p));
+      v[4 * k] = q[0];
+      v[4 * k + 1] = q[1];
+      v[4 * k + 2] = q[2];
+      v[4 * k + 3] = q[3];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 * k + j] = p + j < hi ? c.acc_flow[p + j] : 0xFFFFFFFFu;
+    }
+  }
+  const uint32_t lmax = 0xFFFFFFFFu >> c.pack_bits;
+  bool sat = false;
+#pragma unroll
+  for (int e = 0; e < 4 * U; ++e) {
+    claim[e] = v[e] == 0xFFFFFFFFu ? v[e] : (v[e] & ((1u << c.pack_bits) - 1u));
+    len[e] = v[e] == 0xFFFFFFFFu ? 0u : v[e] >> c.pack_bits;
+    sat |= len[e] == lmax;
+  }
+  if (__any(sat)) {  // a caplen past the packed field: the side array (rare)
+#pragma unroll
+    for (int e = 0; e < 4 * U; ++e)
+      if (len[e] == lmax) len[e] = c.acc_len[p0 + 4ull * (e / 4) * kCountBlock + (e % 4)];
+  }
+}
+
 template <bool PACK>
 __device__ __forceinline__ uint32_t load_claim(const CountArgs& c, uint64_t p) {
   const uint32_t v = __builtin_nontemporal_load(&c.acc_flow[p]);
@@ -1717,7 +1754,7 @@ __device__ uint64_t fused_rank_block(const CountArgs& c, uint32_t* s_map) {
 // Bins are indexed by CLAIM (dense in [0, F)); the record's output id is
 // omap[claim] (the local dense id, or — after a flow-hash exchange — the global
 // one), staged in LDS; k_count_reduce maps claims to local ids for the counters.
-template <int U, int ABL3, bool PACK>
+template <int U, int ABL3, bool PACK, bool VEC = false>
 __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   __shared__ uint64_t s_bin[kCountBins];  // by claim
   __shared__ uint32_t s_map[kCountBins];  // claim index -> output id
@@ -1773,32 +1810,55 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
     atomicAdd((unsigned long long*)&c.cnt[2ull * lid], (unsigned long long)pk);
     atomicAdd((unsigned long long*)&c.cnt[2ull * lid + 1], (unsigned long long)by);
   };
-  for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
-    uint32_t s[U], len[U], id[U];
+  // VEC: four consecutive records per lane and load (packed words only)
+  constexpr int UU = VEC ? 4 * U : U;
+  for (uint64_t base = lo; base < hi; base += (uint64_t)UU * kCountBlock) {
+    uint32_t s[UU], len[UU], id[UU];
     if (kK3LoadPrio) __builtin_amdgcn_s_setprio(kK3LoadPrio);
-    load_acc<U, PACK>(c, base + tid, lo, hi, s, len);  // streamed once: non-temporal
+    if constexpr (VEC) load_acc4<U>(c, base + 4ull * tid, hi, s, len);  // non-temporal
+    else load_acc<U, PACK>(c, base + tid, lo, hi, s, len);  // streamed once: non-temporal
     if (kK3LoadPrio) __builtin_amdgcn_s_setprio(0);
     if (ABL3 & 2) {
 #pragma unroll
-      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : (s[k] & 8191u);
+      for (int k = 0; k < UU; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : (s[k] & 8191u);
     } else if (mode == 0) {
 #pragma unroll
-      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : s_map[s[k]];
+      for (int k = 0; k < UU; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : s_map[s[k]];
     } else {
 #pragma unroll
-      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.omap[s[k]];
+      for (int k = 0; k < UU; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.omap[s[k]];
     }
     if (c.out_id && !(ABL3 & 4)) {
+      if constexpr (VEC) {
+        const uint64_t lim = hi < c.out_cap ? hi : c.out_cap;
 #pragma unroll
-      for (int k = 0; k < U; ++k) {
-        const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
-        if (p < hi && p < c.out_cap) __builtin_nontemporal_store(id[k], &c.out_id[p]);
+        for (int k = 0; k < U; ++k) {
+          const uint64_t p = base + 4ull * ((uint64_t)k * kCountBlock + tid);
+          if (p + 3 < lim) {
+            u32x4 q;
+            q[0] = id[4 * k];
+            q[1] = id[4 * k + 1];
+            q[2] = id[4 * k + 2];
+            q[3] = id[4 * k + 3];
+            __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(c.out_id + p));
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (p + j < lim) c.out_id[p + j] = id[4 * k + j];
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+          const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
+          if (p < hi && p < c.out_cap) __builtin_nontemporal_store(id[k], &c.out_id[p]);
+        }
       }
     }
     if (ABL3 & 1) {
       uint32_t x = 0;
 #pragma unroll
-      for (int k = 0; k < U; ++k) x ^= id[k] ^ len[k];
+      for (int k = 0; k < UU; ++k) x ^= id[k] ^ len[k];
       asm volatile("" ::"v"(x));
       continue;
     }
@@ -1808,20 +1868,20 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
       bool same = s0 != 0xFFFFFFFFu;
       uint32_t nk = 0, sl = 0;
 #pragma unroll
-      for (int k = 0; k < U; ++k) {
+      for (int k = 0; k < UU; ++k) {
         const bool v = s[k] != 0xFFFFFFFFu;
         same = same && (!v || (s[k] == s0 && len[k] < kBigLen));
         nk += v ? 1u : 0u;
         sl += v ? len[k] : 0u;
       }
       if (__all(same)) {
-        // pk <= 64*U, by <= 64*U*(kBigLen-1) < 2^32
-        const uint32_t pk = wave_sum32(nk), by = wave_sum32(sl);
+        // pk <= 64*UU, by <= 64*UU*(kBigLen-1) < 2^32 at UU <= 32 (sums in 64 bits)
+        const uint64_t pk = wave_sum64(nk), by = wave_sum64(sl);
         if (lane == 0)
           atomicAdd((unsigned long long*)&s_bin[s0], ((unsigned long long)pk << kBinPkShift) | by);
       } else {
 #pragma unroll
-        for (int k = 0; k < U; ++k) {
+        for (int k = 0; k < UU; ++k) {
           if (s[k] == 0xFFFFFFFFu) continue;
           if (len[k] < kBigLen)
             atomicAdd((unsigned long long*)&s_bin[s[k]], (1ull << kBinPkShift) | len[k]);
@@ -1831,7 +1891,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < U; ++k) {
+      for (int k = 0; k < UU; ++k) {
         const bool mine = s[k] != 0xFFFFFFFFu;
         const uint64_t am = __ballot(mine);
         const uint32_t leader = am ? (uint32_t)__ffsll((unsigned long long)am) - 1 : 0u;
@@ -3171,6 +3231,12 @@ static void launch_count_variant(const CountArgs& c, unsigned g1, unsigned g1s, 
     case 7: KC(8, 7); break;
     case 16: KC(16, 0); break;
     case 32: KC(4, 0); break;
+    case 40:  // 16-B loads of four packed words per lane: U = 4 / 2 loads per lane
+    case 42:  // (U = 8 spills 328 VGPRs)
+      if (c.pack_bits && k3v == 40) hipLaunchKernelGGL((k_count<4, 0, true, true>), grid, dim3(kCountBlock), 0, s, c);
+      else if (c.pack_bits) hipLaunchKernelGGL((k_count<2, 0, true, true>), grid, dim3(kCountBlock), 0, s, c);
+      else KC(8, 0);
+      break;
     default: KC(8, 0); break;
   }
 #undef KC

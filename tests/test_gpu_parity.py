@@ -792,3 +792,25 @@ def test_max_wide_flows_exact_bound(gpu, oracle, short):
         assert len(keys) == short and wide[keys].all()
         assert res.flow_id[~refused].max() < len(table) - short
         assert not np.isin(fi[~refused], keys).any()
+
+
+@pytest.mark.parametrize("k3v", ["40", "42"])
+@pytest.mark.parametrize("flows", [1, 40, 5000])
+def test_k3_vector_loads_variant(gpu, oracle, flows, k3v, monkeypatch):
+    """K3 mode 0 with 16-B loads of four packed K1 -> K3 words per lane (variants
+    build, TCBEE_K3ABL=40/42: 4 / 2 loads per lane): a ragged tail (scalar fallback),
+    saturated packed caplens (the side array), > 64 KiB frames (device atomics), a
+    hot flow (the wave-uniform add) — bit-exact vs the oracle."""
+    from tracegen import mixed_trace
+    monkeypatch.setenv("TCBEE_K3ABL", k3v)
+    tr = mixed_trace(150_001, seed=303, n_flows=flows)
+    rng = np.random.default_rng(8)
+    big = rng.choice(tr.n, size=300, replace=False)
+    pad = 2_600_000
+    ln = tr.caplen.copy()
+    ln[big] = rng.integers(16_000, pad, size=len(big)).astype(np.uint32)
+    tr2 = Trace(np.concatenate([tr.arena, np.zeros(pad, np.uint8)]), tr.offset, ln, tr.ts_ns)
+    with tcbee_amd.PacketParser(max_frames=1 << 18, max_arena=1 << 27, max_flows=1 << 13,
+                                variants=True) as p:
+        assert_same(p.parse(tr2), oracle.parse(tr2), p.flows())
+        assert p.status() == 0 and p.count_mode() == 0
