@@ -83,15 +83,16 @@ struct PersistState {
   uint64_t wide_claims;  // wide-slot keys claimed (bounded by FlowTable::max_wide)
 };
 
-// Zeroed before every batch (one 32-B memset).
+// Zeroed before every batch (k_prep).
 struct BatchState {
   uint64_t n_acc;       // accepted frames in this batch (last tile writes it)
   uint64_t n_new;       // flows first claimed in this batch
   uint64_t flow_total;  // flows with ids after this batch (rank step writes it)
   uint64_t fs_max_word; // highest first-seen bitmap word set this batch (bounds the
                         // rank scan; the words up to it are cleared again by K3)
+  uint64_t k3_done;     // (fused rank) K3 blocks finished: the last one advances the bases
 };
-static_assert(sizeof(BatchState) == 32, "memset size");
+static_assert(sizeof(BatchState) == 40, "memset size");
 
 struct PrepArgs {
   BatchState* batch;

@@ -1056,7 +1056,7 @@ __global__ void k_table_init(FlowTable t) {
 __global__ void k_prep(PrepArgs p) {
   const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  if (t0 < 4) reinterpret_cast<uint64_t*>(p.batch)[t0] = 0;
+  if (t0 < sizeof(BatchState) / 8) reinterpret_cast<uint64_t*>(p.batch)[t0] = 0;
   for (uint64_t i = t0; i < p.ntiles; i += stride) p.tile_status[i] = 0;
   // (the first-seen bitmap is not swept here: it is all zero between batches —
   //  K3 clears the words the rank step set)
@@ -1722,10 +1722,11 @@ __device__ void count_ranges(const CountArgs& c, uint64_t n_acc, uint64_t nflows
 // n_new). The new ids' counters were zeroed by k_prep (zero_free_counters): every
 // block may add a big frame to them, and nothing orders those adds after a zeroing
 // here. Returns the flow count after the batch.
-__device__ uint64_t fused_rank_block(const CountArgs& c, uint32_t* s_map) {
+__device__ uint64_t fused_rank_block(const CountArgs& c, uint32_t* s_map, uint64_t& fbase_out) {
   __shared__ uint32_t s_nfs[kFuseRankMax];
   const uint32_t tid = threadIdx.x;
   const uint64_t base = c.persist->rec_base, fbase = c.persist->flow_count;
+  fbase_out = fbase;
   const uint64_t room = c.tab.max_claims > fbase ? c.tab.max_claims - fbase : 0;
   const uint64_t n_new = c.batch->n_new < room ? c.batch->n_new : room;
   for (uint32_t j = tid; j < n_new; j += kCountBlock)
@@ -1761,7 +1762,8 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint64_t n_acc = c.batch->n_acc;
   // (fused rank: K2 did not run; the flow count is this block's own)
-  const uint64_t nflows = c.fused_rank ? fused_rank_block(c, s_map) : c.batch->flow_total;
+  uint64_t fbase_f = 0;
+  const uint64_t nflows = c.fused_rank ? fused_rank_block(c, s_map, fbase_f) : c.batch->flow_total;
   if (blockIdx.x == 0 && tid == 0) {
     // finalize (nothing here writes what other blocks read: with a fused rank every
     // block reads the old record base / flow count, which the reduce advances)
@@ -1795,7 +1797,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   }
   if (mode == 0) {
     // (fused rank: claims of this batch's new flows were mapped above)
-    const uint64_t mapped = c.fused_rank ? c.persist->flow_count : nflows;
+    const uint64_t mapped = c.fused_rank ? fbase_f : nflows;
     for (uint32_t b = tid; b < nflows; b += kCountBlock) {
       s_bin[b] = 0;
       if (b < mapped) s_map[b] = c.omap[b];
@@ -1905,7 +1907,26 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
       }
     }
   }
-  if (mode == 0) {
+  if (mode == 0 && c.fused_rank) {
+    // (fused rank, <= kFuseRankMax flows: no reduce launch) the block's bins go
+    // straight to the counters by local id — at most 2 x 256 device adds per block —
+    // and the last block to finish advances the record base / flow count: every
+    // block has read (and used) the old ones by now
+    __syncthreads();
+    for (uint32_t b = tid; b < nflows; b += kCountBlock) {
+      const uint64_t v = s_bin[b];
+      if (v) {
+        const uint32_t id = s_map[b];
+        atomicAdd((unsigned long long*)&c.cnt[2ull * id], (unsigned long long)(v >> kBinPkShift));
+        atomicAdd((unsigned long long*)&c.cnt[2ull * id + 1], (unsigned long long)(v & kBinByMask));
+      }
+    }
+    if (tid == 0 &&
+        atomicAdd((unsigned long long*)&c.batch_rw->k3_done, 1ull) == (unsigned long long)gridDim.x - 1) {
+      c.persist_rw->rec_base += n_acc;
+      c.persist_rw->flow_count = nflows;
+    }
+  } else if (mode == 0) {
     // per-block partial histogram, dense and coalesced; k_count_reduce sums them
     // (one writer per flow: no device-scope atomics)
     __syncthreads();
@@ -3330,7 +3351,9 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
   // mode 0 needs kCountBins threads; mode 1 up to nb_max * kBucket (grid-stride)
   // (1024-thread blocks: mode 0 takes 64 claims per block, its 16 waves split the rows)
   const unsigned gr = (g2 || c.range_ok) ? 256u : (unsigned)(kCountBins / 256);
-  hipLaunchKernelGGL(k_count_reduce, dim3(gr), dim3(64 * kReduceWaves), 0, s, c, g1, g2);  // g1: mode-0 rows
+  // (a fused-rank batch has no reduce: k_count adds its bins and advances the bases)
+  if (!c.fused_rank)
+    hipLaunchKernelGGL(k_count_reduce, dim3(gr), dim3(64 * kReduceWaves), 0, s, c, g1, g2);  // g1: mode-0 rows
   return hipGetLastError();
 }
 
