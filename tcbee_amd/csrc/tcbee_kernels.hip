@@ -66,6 +66,15 @@ constexpr int kK1LoadPrio = TCBEE_K1_LOAD_PRIO;
 #define TCBEE_K3_LOAD_PRIO 0
 #endif
 constexpr int kK3LoadPrio = TCBEE_K3_LOAD_PRIO;
+// K1: a probe that misses its plain-load snapshot (a new flow, a slot still BUSY
+// with another lane's insert, a stale line) takes flow_upsert's coherent path
+// AFTER the tile's records are stored instead of before (the spin on a BUSY slot
+// then overlaps the record work; a cold table's first tiles all wait on a few
+// inserts). Build-time A/B knob (tools/lib_ab.sh, HIPEXTRA=-D...).
+#ifndef TCBEE_K1_DEFER_UPSERT
+#define TCBEE_K1_DEFER_UPSERT 0
+#endif
+constexpr bool kDeferUpsert = TCBEE_K1_DEFER_UPSERT != 0;
 [[maybe_unused]] constexpr int kAuxSc1 = 16;  // buffer cache-policy bits: sc1 (agent coherence, bypass L1)
 constexpr int kAuxPlain = 0;  // plain: L1/L2 allocating
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -782,10 +791,28 @@ void k_parse(ParseArgs a) {
   const bool withhold = a.withhold_every && (tile % a.withhold_every) == a.withhold_every - 1;
   if (!(ABL & 1) && !withhold && tid == 0) lookback_publish(a.tile_status, tile, total);
 
+  // probe results per frame group (lane-private until publish_probe shares a
+  // wave-uniform key's leader result with its wave)
+  uint32_t psl[FPL], pcl[FPL], pfs[FPL];
+  bool pend[FPL], uni[FPL], want[FPL];
+  uint32_t leader[FPL];
+  uint64_t h[FPL];
+#pragma unroll
+  for (int f = 0; f < FPL; ++f) pend[f] = uni[f] = want[f] = false;
+  auto publish_probe = [&](int f) {
+    if (uni[f]) {
+      slot[f] = __shfl(psl[f], leader[f]);
+      claim[f] = __shfl(pcl[f], leader[f]);
+      fs_seen[f] = __shfl(pfs[f], leader[f]);
+    } else if (acc[f]) {
+      slot[f] = psl[f];
+      claim[f] = psl[f] == 0xFFFFFFFFu ? 0xFFFFFFFFu : pcl[f];
+      fs_seen[f] = pfs[f];
+    }
+  };
   if (FLOWS) {
     // phase B: hash, then issue the first probe's loads of every frame: an IPv4-form
     // key's 16-B compact slot + its fs32 (one line), any other key's 64-B wide slot
-    uint64_t h[FPL];
     u32x4 Q[FPL][4];
     uint32_t FS[FPL], S0[FPL];
     bool v4k[FPL];
@@ -795,8 +822,6 @@ void k_parse(ParseArgs a) {
         a.tab.slots, 0, (int)(uint32_t)(a.tab.nlines * 64u), 0x00020000);
     const __amdgpu_buffer_rsrc_t wd_rs = __builtin_amdgcn_make_buffer_rsrc(
         a.tab.wide, 0, (int)(uint32_t)((a.tab.wide_mask + 1) * 64u), 0x00020000);
-    bool uni[FPL], want[FPL];
-    uint32_t leader[FPL];
 #pragma unroll
     for (int f = 0; f < FPL; ++f) {
       const uint64_t am = __ballot(acc[f]);
@@ -909,19 +934,15 @@ void k_parse(ParseArgs a) {
             }
           }
         }
-        if (slow)
+        if (slow && !kDeferUpsert)
           sl = flow_upsert(a.tab, K[f], h[f], a.batch, a.new_list, a.persist, fbase, fs, cl,
                            kFs32Flag | (uint32_t)(i0 + (uint64_t)f * BLK + tid));
+        pend[f] = slow && kDeferUpsert;
       }
-      if (uni[f]) {
-        slot[f] = __shfl(sl, leader[f]);
-        claim[f] = __shfl(cl, leader[f]);
-        fs_seen[f] = __shfl(fs, leader[f]);
-      } else if (acc[f]) {
-        slot[f] = sl;
-        claim[f] = sl == 0xFFFFFFFFu ? 0xFFFFFFFFu : cl;
-        fs_seen[f] = fs;
-      }
+      psl[f] = sl;
+      pcl[f] = cl;
+      pfs[f] = fs;
+      if (!kDeferUpsert) publish_probe(f);
     }
   }
   if (!(ABL & 2)) {
@@ -971,6 +992,17 @@ void k_parse(ParseArgs a) {
           wave_lds_sync();
         }
       }
+    }
+  }
+
+  if (FLOWS && kDeferUpsert) {
+    // the probes whose snapshot missed, after the records are out
+#pragma unroll
+    for (int f = 0; f < FPL; ++f) {
+      if (want[f] && pend[f])
+        psl[f] = flow_upsert(a.tab, K[f], h[f], a.batch, a.new_list, a.persist, fbase, pfs[f],
+                             pcl[f], kFs32Flag | (uint32_t)(i0 + (uint64_t)f * BLK + tid));
+      publish_probe(f);
     }
   }
 

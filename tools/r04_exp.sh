@@ -18,8 +18,8 @@ step() {  # name timeout cmd...
 }
 for s in "$@"; do
   case $s in
-    ab)  step ab 800 env NAMES="${NAMES:-wt_prio3 wt_k3prio2 wt_prio1}" PAIRS=2 bash tools/ab_multi.sh \
-           --workloads imix10k,imix1M --rounds 3 --iters 5 ;;
+    ab)  step ab 1000 env NAMES="${NAMES:-wt_prio3 wt_defer wt_k3prio2}" PAIRS=2 bash tools/ab_multi.sh \
+           --workloads imix10k,imix1M,64B1 --rounds 3 --iters 5 ;;
     k3v) step k3v 400 python tools/k1_sweep.py --fpl 2 --flows-only --workloads imix10k,64B1 \
            --var TCBEE_K3ABL=0,40,42 --rounds 3 --iters 5 ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
