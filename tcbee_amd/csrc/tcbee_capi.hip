@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <utility>
 #include <vector>
 
 #include "../../include/tcbee_amd.h"
@@ -33,6 +34,17 @@ struct tcbee_ctx {
   FlowTable tab{};
   uint64_t nlines = 0;  // flow-table slot lines (6 slots of 16 B each)
   PersistState* d_persist = nullptr;
+  // Small contexts (max_flows <= kFuseRankMax): two table generations (slot units,
+  // wide slots, counters, persist state; the per-claim key / first_seen / id arrays
+  // are shared), so that a reset is a switch to the other, already empty generation
+  // and a fused batch needs no k_prep launch: its K3 empties the inactive
+  // generation, zeroes the tile words and the next batch's state slot (round 4)
+  bool small_gen = false;
+  FlowTable tab_alt{};
+  PersistState* d_persist_alt = nullptr;
+  bool alt_clean = true;    // the inactive generation is empty (or being emptied in order)
+  bool prepped = false;     // the last batch's K3 prepared the next one (tile words, slot)
+  uint64_t tiles_hw = 0;    // tile words used since they were all last zeroed
   BatchState* d_batch = nullptr;     // = d_batch_slot[slot] of the current batch
   // two slots of what a batch's K3 reads (batch state, K1 -> K3 scratch), so that
   // with TCBEE_EX_ASYNC_IDS batch i's K3 (ids stream) runs beside batch i+1's K1;
@@ -196,6 +208,13 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
   dfree(c->tab.cnt);
   dfree(c->tab.cmap);
   dfree(c->d_persist);
+  if (c->small_gen) {  // (the alt generation's own arrays; ent / cfs / cmap are shared)
+    dfree(c->tab_alt.slots);
+    dfree(c->tab_alt.wide);
+    dfree(c->tab_alt.wide_used);
+    dfree(c->tab_alt.cnt);
+    dfree(c->d_persist_alt);
+  }
   if (c->k3_async && c->ev_k3) (void)hipEventSynchronize(c->ev_k3);
   for (int i = 0; i < 2; ++i) {
     dfree(c->d_batch_slot[i]);
@@ -333,6 +352,9 @@ int tcbee_ctx_create_ex(tcbee_ctx** out, int device, uint64_t max_frames, uint64
     if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
       return fail(map_err(e));
   if ((e = dalloc(&c->d_tile_status, c->max_tiles)) != hipSuccess) return fail(map_err(e));
+  // all zero between batches of small contexts (their K3 re-zeroes the words a batch used)
+  if ((e = hipMemset(c->d_tile_status, 0, c->max_tiles * sizeof(uint64_t))) != hipSuccess)
+    return fail(map_err(e));
   if ((e = dalloc(&c->d_new_list, c->max_flows)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_bitmap, c->max_words)) != hipSuccess) return fail(map_err(e));
   // all zero between batches from here on (K3 clears the words a batch set)
@@ -382,6 +404,30 @@ int tcbee_ctx_create_ex(tcbee_ctx** out, int device, uint64_t max_frames, uint64
     if ((e = dalloc(&c->d_k3_coffs, ((max_frames + kChunkMin - 1) / kChunkMin + 1) * (kChunkMaxNb + 1))) !=
         hipSuccess)
       return fail(map_err(e));
+  }
+  if (c->max_flows <= kFuseRankMax) {
+    // the second table generation and the second batch-state slot (K1 -> K3 scratch
+    // of both slots too: batches alternate slots from now on)
+    c->small_gen = true;
+    c->tab_alt = c->tab;
+    c->tab_alt.slots = nullptr;
+    c->tab_alt.wide = nullptr;
+    c->tab_alt.wide_used = nullptr;
+    c->tab_alt.cnt = nullptr;
+    if ((e = dalloc(&c->tab_alt.slots, 8 * c->nlines)) != hipSuccess) return fail(map_err(e));
+    if ((e = dalloc(&c->tab_alt.wide, 8 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
+    if ((e = hipMemset(c->tab_alt.wide, 0xFF, 64 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
+    if ((e = hipMemset2D(c->tab_alt.wide, 64, 0, 8, c->tab.wide_mask + 1)) != hipSuccess) return fail(map_err(e));
+    if ((e = dalloc(&c->tab_alt.wide_used, 1)) != hipSuccess) return fail(map_err(e));
+    if ((e = hipMemset(c->tab_alt.wide_used, 0, 4)) != hipSuccess) return fail(map_err(e));
+    if ((e = dalloc(&c->tab_alt.cnt, 2 * c->max_flows)) != hipSuccess) return fail(map_err(e));
+    if ((e = dalloc(&c->d_persist_alt, 1)) != hipSuccess) return fail(map_err(e));
+    if ((e = hipMemset(c->d_persist_alt, 0, sizeof(PersistState))) != hipSuccess) return fail(map_err(e));
+    if ((e = launch_table_init(c->tab_alt, c->stream)) != hipSuccess) return fail(map_err(e));
+    if ((e = dalloc(&c->d_batch_slot[1], 1)) != hipSuccess) return fail(map_err(e));
+    if ((e = dalloc(&c->d_slot_scratch_s[1], c->max_frames)) != hipSuccess) return fail(map_err(e));
+    if ((e = dalloc(&c->d_len_scratch_s[1], c->max_frames)) != hipSuccess) return fail(map_err(e));
+    c->nslot = 2;
   }
   rc = tcbee_flow_reset(c);
   if (rc != TCBEE_OK) return fail(rc);
@@ -479,7 +525,25 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
   // themselves (one launch fewer per batch; config 2: 1M frames of one flow)
   const bool fuse = flows && ntiles > 0 && nwords <= kRankSmallWords && c->max_flows <= kFuseRankMax &&
                     !defer && !async && !c->no_fuse_rank;
-  {
+  // small contexts: no k_prep launch when the previous batch's K3 prepared this one
+  // (tile words and this slot zero) and the table needs no reset, or the reset is a
+  // switch to the other generation, which that K3 emptied
+  const bool gen = c->small_gen && fuse;
+  bool skip_prep = false;
+  if (gen && c->prepped) {
+    if (!c->reset_pending) {
+      skip_prep = true;
+    } else if (c->alt_clean) {
+      std::swap(c->tab, c->tab_alt);
+      std::swap(c->d_persist, c->d_persist_alt);
+      c->reset_pending = false;
+      c->alt_clean = false;  // the old generation: emptied by this batch's K3
+      skip_prep = true;
+    }
+  }
+  c->prepped = false;  // (set again below when this batch's K3 prepares the next one)
+  if (c->tiles_hw < ntiles) c->tiles_hw = ntiles;
+  if (!skip_prep) {
     PrepArgs pa{};
     pa.batch = c->d_batch;
     pa.tile_status = c->d_tile_status;
@@ -580,6 +644,14 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     // workgroup per CU); 92: its 8192-record form (512 threads, two per CU) — slower
     // in round 2 than 16384: 125k flows 5.60 vs 5.72 ms/step, 1M flows 7.51 vs 7.77
     k.chunk = (c->k3_variant == 92 || c->k3_variant == 95) ? 8192u : c->k3_variant == 93 ? 16384u : 12288u;
+    if (gen) {  // this K3 prepares the next batch (see skip_prep above)
+      k.clean_tiles = c->d_tile_status;
+      k.clean_ntiles = c->tiles_hw;
+      k.next_batch = c->d_batch_slot[c->slot ^ 1];
+      k.clean_alt = c->alt_clean ? 0u : 1u;
+      k.alt = c->tab_alt;
+      k.alt_persist = c->d_persist_alt;
+    }
     // trade-off: more blocks = more latency hidden; each block writes a partial row
     // of every flow, so a block should see a few thousand records; and a block
     // never covers more than kK3MaxPer records (bin fields cannot overflow)
@@ -628,6 +700,11 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
                          c->k3_variant));
     if (async) TRY_HIP(hipEventRecord(c->ev_k3, ks));
     c->k3_async = async;
+    if (gen) {
+      c->prepped = true;
+      c->alt_clean = true;  // (emptied by this K3, stream-ordered before any later use)
+      c->tiles_hw = 0;
+    }
   } else {
     TRY_HIP(launch_finalize(c->d_batch, c->d_persist, out_cap, out_n_dev, ctr_dev, cfg->direction, s));
     if (defer) {  // keep the parse -> finish pairing of a deferred batch
@@ -937,6 +1014,7 @@ int tcbee_flow_set_first_seen_device(tcbee_ctx* c, const uint64_t* fs_by_id_dev,
 int tcbee_flow_merge_device(tcbee_ctx* c, const tcbee_flow_entry* ent_dev, uint64_t nseg,
                             uint64_t stride, const uint64_t* seg_meta_dev,
                             uint64_t max_total_records, uint32_t* out_ids_dev, void* stream) {
+  if (c) c->prepped = false;  // (rank kernels on the current slot; the next batch preps)
   if (!c || !seg_meta_dev || (nseg * stride && (!ent_dev || !out_ids_dev))) return TCBEE_EINVAL;
   // merged first_seen values are min-reduced in the slots' 31-bit fs32 words
   if (max_total_records >= (1ull << 31)) return TCBEE_ECAPACITY;

@@ -198,6 +198,16 @@ struct CountArgs {
   const uint64_t* new_list;  // (fused rank) slots first claimed this batch
   BatchState* batch_rw;      // (fused rank) the batch state K2 would have written
   FlowTable tab;             // (fused rank) slot fs32 words, cfs, cmap
+  // (fused rank, small contexts: the next batch needs no k_prep launch) K3 also
+  // leaves what k_prep would have prepared: tile status words [0, clean_ntiles)
+  // zero, the next batch's state slot zero, and — after a reset switched the
+  // context to its other table generation — the now-inactive generation empty
+  uint64_t* clean_tiles;
+  uint64_t clean_ntiles;
+  BatchState* next_batch;
+  uint32_t clean_alt;
+  FlowTable alt;             // the inactive generation: slot units, wide slots, counters
+  PersistState* alt_persist;
 };
 constexpr uint64_t kFuseRankMax = 256;
 // g1 = k_count blocks; g1s = k_count_scatter blocks; g2 = k_count_bucket blocks

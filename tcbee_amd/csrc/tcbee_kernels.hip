@@ -1939,6 +1939,20 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
       }
     }
   }
+  if (c.next_batch) {
+    // (small contexts) the next batch's preparation, grid-strided: nothing here is
+    // read by this launch (this batch's K1 is done with its tile words; the next
+    // slot and the inactive generation are untouched by this batch)
+    const uint64_t t0 = blockIdx.x * (uint64_t)kCountBlock + tid;
+    const uint64_t stride = (uint64_t)gridDim.x * kCountBlock;
+    for (uint64_t i = t0; i < c.clean_ntiles; i += stride) c.clean_tiles[i] = 0;
+    if (t0 < sizeof(BatchState) / 8) reinterpret_cast<uint64_t*>(c.next_batch)[t0] = 0;
+    if (c.clean_alt) {
+      if (t0 < sizeof(PersistState) / 8) reinterpret_cast<uint64_t*>(c.alt_persist)[t0] = 0;
+      empty_units(c.alt, t0, stride);
+      for (uint64_t i = t0; i < 2 * c.alt.max_claims; i += stride) c.alt.cnt[i] = 0;
+    }
+  }
   if (mode == 0 && c.fused_rank) {
     // (fused rank, <= kFuseRankMax flows: no reduce launch) the block's bins go
     // straight to the counters by local id — at most 2 x 256 device adds per block —

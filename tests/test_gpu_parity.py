@@ -815,3 +815,48 @@ def test_k3_vector_loads_variant(gpu, oracle, flows, k3v, monkeypatch):
                                 variants=True) as p:
         assert_same(p.parse(tr2), oracle.parse(tr2), p.flows())
         assert p.status() == 0 and p.count_mode() == 0
+
+
+def test_small_context_generations_and_prep_free_batches(gpu, oracle):
+    """Round 4: a small context (<= 256 flows) keeps two table generations; a fused
+    batch's K3 prepares the next batch (tile words, state slot) and empties the
+    inactive generation, so the next batch has no k_prep launch and a reset is a
+    switch of generation. A sequence mixing resets, kept tables, IPv6 keys (wide
+    slots), frames of >= 64 KiB, table reads between batches, an empty batch, a
+    no-flows batch, a sync reset and batches of different tile counts, each checked
+    against the oracle (records, hashes, ids, counters, the table)."""
+    from tracegen import mixed_trace
+    tr = mixed_trace(60_000, seed=1212, n_flows=24)
+    rng = np.random.default_rng(3)
+    ln = tr.caplen.copy()
+    big = rng.choice(tr.n, size=200, replace=False)
+    ln[big] = rng.integers(65_536, 70_001, size=len(big)).astype(np.uint32)
+    tr = Trace(np.concatenate([tr.arena, np.zeros(80_000, np.uint8)]), tr.offset, ln, tr.ts_ns)
+    assert len(oracle.parse(tr)[4]) <= 256
+    cuts = [(0, 20_000), (20_000, 21_000), (21_000, 60_000), (5_000, 5_000), (100, 7_000),
+            (7_000, 59_999), (0, 60_000), (33, 34), (1_000, 45_000)]
+    # per step: reset before? ('dev' = tcbee_flow_reset_device, 'sync', None), flows on?
+    plan = [("dev", True), ("dev", True), (None, True), ("dev", True), (None, True),
+            ("sync", True), ("dev", False), ("dev", True), (None, True)]
+    with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 27, max_flows=256) as p:
+        ft = oracle.new_flowtab()
+        base = 0
+        try:
+            for (lo, hi), (reset, flows) in zip(cuts, plan):
+                if reset:
+                    p.reset_flows(sync=reset == "sync")
+                    oracle.free_flowtab(ft)
+                    ft = oracle.new_flowtab()
+                    base = 0
+                part = tr.slice(lo, hi)
+                res = p.parse(part, flows=flows)
+                orc = oracle.parse(part, ft=ft if flows else None, record_base=base, flows=flows)
+                if flows:
+                    assert_same(res, orc)
+                    base += len(orc[0])
+                    assert np.array_equal(p.flows(), oracle.flows(ft))
+                else:
+                    assert np.array_equal(res.records, orc[0]) and res.counters == orc[3]
+                assert p.status() == 0
+        finally:
+            oracle.free_flowtab(ft)
