@@ -22,7 +22,7 @@ for s in "$@"; do
            --workloads imix10k,imix1M,64B1 --rounds 3 --iters 5 ;;
     k3v) step k3v 400 python tools/k1_sweep.py --fpl 2 --flows-only --workloads imix10k,64B1 \
            --var TCBEE_K3ABL=0,40,42 --rounds 3 --iters 5 ;;
-    c2ab) step c2ab 600 env NAMES="${NAMES:-wt_defer}" PAIRS=3 bash tools/ab_multi.sh \
+    c2ab) step c2ab 600 env NAMES="${NAMES:-HEAD~1}" PAIRS=3 bash tools/ab_multi.sh \
            --frames 1000000 --workloads 64B1,imix10k --rounds 5 --iters 20 --min-table 64 ;;
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread \
              > gpurun_out/pytest_gpu.log 2>&1
