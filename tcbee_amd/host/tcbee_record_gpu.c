@@ -14,6 +14,7 @@
  *   tcbee-record-gpu [--tc] [--port P] [--db PATH] [--window W] [--threads T] PCAP PREFIX
  * Prints one JSON line: frames, records, flows, counters, seconds.
  */
+#define _POSIX_C_SOURCE 199309L  /* clock_gettime */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>

@@ -24,14 +24,15 @@ def _ensure_built():
     if not os.path.exists(oracle_so):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
                        stdout=subprocess.DEVNULL)
-    host_so = os.path.join(ROOT, "tcbee_amd", "lib", "libtcbee_host.so")
-    if not os.path.exists(host_so):
-        subprocess.run(["make", "-C", os.path.join(ROOT, "tcbee_amd", "host")], check=True,
-                       stdout=subprocess.DEVNULL)
     libs = [os.path.join(ROOT, "tcbee_amd", "lib", n)
             for n in ("libtcbee_amd.so", "libtcbee_amd_variants.so")]
     if not all(os.path.exists(x) for x in libs):
         subprocess.run(["make", "-C", os.path.join(ROOT, "tcbee_amd", "csrc")], check=True,
+                       stdout=subprocess.DEVNULL)
+    host = [os.path.join(ROOT, "tcbee_amd", "lib", "libtcbee_host.so"),
+            os.path.join(ROOT, "tcbee_amd", "bin", "tcbee-record-gpu")]
+    if not all(os.path.exists(x) for x in host):  # (the C host program links both)
+        subprocess.run(["make", "-C", os.path.join(ROOT, "tcbee_amd", "host")], check=True,
                        stdout=subprocess.DEVNULL)
 
 

@@ -244,3 +244,33 @@ def test_config1_loopback_iperf3_replay(gpu, oracle, tmp_path):
                                                               got["flows"][0][3], 5201, 6]
     m = json.load(open(prefix + "metrics.json"))
     assert m["egress"] == t_in.n and m["handled"] == t_in.n
+
+
+@pytest.mark.parametrize("egress,port", [(False, 0), (True, 5201)])
+def test_compiled_c_host_replay(gpu, oracle, tmp_path, egress, port):
+    """tcbee-record-gpu: a compiled C program over the two C ABIs only (no Python in
+    the process) — pcap -> tcbee_pipe -> <prefix>xdp.tcp / tc.tcp through the
+    buffered .tcp writer -> metrics.json -> the tcbee-process stage into SQLite; the
+    bytes, the counters and the database equal the oracle path's (both hooks,
+    FILTER_PORT)."""
+    import subprocess
+    exe = os.path.join(ROOT, "tcbee_amd", "bin", "tcbee-record-gpu")
+    t = mixed_trace(40_000, seed=88, n_flows=60)
+    pcap = str(tmp_path / "trace.pcap")
+    host.write_pcap(pcap, t)
+    prefix = str(tmp_path) + "/c_"
+    db = str(tmp_path / "c.sqlite")
+    args = [exe, "--port", str(port), "--db", db, "--threads", "4"] + (["--tc"] if egress else [])
+    r = subprocess.run(args + [pcap, prefix], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    rec, fh, fi, ctr, table = oracle.parse(t, filter_port=port, direction=int(egress))
+    assert out["frames"] == t.n and out["records"] == len(rec) and out["flows"] == len(table)
+    assert {k: out[k] for k in ("ingress", "egress", "handled", "dropped")} == ctr
+    name = "tc.tcp" if egress else "xdp.tcp"
+    assert open(prefix + name, "rb").read() == rec.tobytes()
+    m = json.load(open(prefix + "metrics.json"))
+    assert m == {"handled": ctr["handled"], "dropped": ctr["dropped"], "ingress": ctr["ingress"],
+                 "egress": ctr["egress"], "ingress_calls": 0, "egress_calls": 0}
+    process_ref.process_records(rec.tobytes(), str(tmp_path / "orc.sqlite"))
+    assert process_ref.dump_db(db) == process_ref.dump_db(str(tmp_path / "orc.sqlite"))

@@ -410,3 +410,20 @@ def test_config1_loopback_trace_through_sink(oracle, tmp_path):
     assert [r[1:] for r in got["flows"]][0][3:] == [5201, 6]
     names = {r[2] for r in got["time_series"]}
     assert not any(n.startswith("FLAG_") for n in names)
+
+
+def test_compiled_c_host_builds_and_refuses_without_gpu(tmp_path):
+    """tcbee-record-gpu (tcbee_amd/host/tcbee_record_gpu.c) links against the two C
+    ABIs only; usage errors exit 2, and without a GPU the pipe creation fails loudly
+    (exit 1, the ABI's error text) instead of falling back to anything."""
+    import subprocess
+    exe = os.path.join(ROOT, "tcbee_amd", "bin", "tcbee-record-gpu")
+    assert os.access(exe, os.X_OK)
+    assert subprocess.run([exe], capture_output=True).returncode == 2
+    if tcbee_amd.device_count() > 0:
+        pytest.skip("GPU present (tests/test_gpu_pipeline.py runs it)")
+    tr = tcbee_amd.synth_trace(100, sizes="64")
+    pcap = str(tmp_path / "t.pcap")
+    host.write_pcap(pcap, tr)
+    r = subprocess.run([exe, pcap, str(tmp_path) + "/x_"], capture_output=True, text=True)
+    assert r.returncode == 1 and "pipe_create" in r.stderr
