@@ -1758,15 +1758,11 @@ __device__ uint64_t fused_rank_block(const CountArgs& c, uint32_t* s_map, uint64
   __shared__ uint32_t s_nfs[kFuseRankMax];
   const uint32_t tid = threadIdx.x;
   const uint64_t base = c.persist->rec_base, fbase = c.persist->flow_count;
-  // (the new-flow list is read speculatively beside the bases: in bounds for every
-  //  thread below max_claims <= kFuseRankMax, used below n_new — one round trip less)
-  const uint32_t sl = tid < c.tab.max_claims ? (uint32_t)c.new_list[tid] : 0u;
-  const uint64_t nn = c.batch->n_new;
   fbase_out = fbase;
   const uint64_t room = c.tab.max_claims > fbase ? c.tab.max_claims - fbase : 0;
-  const uint64_t n_new = nn < room ? nn : room;
-  static_assert(kFuseRankMax <= kCountBlock, "one new flow per thread");
-  if (tid < n_new) s_nfs[tid] = *slot_fs_any(c.tab, sl);
+  const uint64_t n_new = c.batch->n_new < room ? c.batch->n_new : room;
+  for (uint32_t j = tid; j < n_new; j += kCountBlock)
+    s_nfs[j] = *slot_fs_any(c.tab, (uint32_t)c.new_list[j]);
   __syncthreads();
   for (uint32_t j = tid; j < n_new; j += kCountBlock) {
     const uint32_t v = s_nfs[j];
@@ -1797,14 +1793,6 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   __shared__ uint32_t s_map[kCountBins];  // claim index -> output id
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint64_t n_acc = c.batch->n_acc;
-  const uint64_t per = count_per(n_acc, gridDim.x);
-  const uint64_t lo = (uint64_t)blockIdx.x * per < n_acc ? (uint64_t)blockIdx.x * per : n_acc;
-  const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
-  // (fused rank: mode 0 is certain, so the block's first records are loaded before the
-  //  rank's dependent loads instead of after them — small batches are latency bound)
-  uint32_t pre_s[U], pre_len[U];
-  const bool pre = !VEC && c.fused_rank;
-  if (pre) load_acc<U, PACK>(c, lo + tid, lo, hi, pre_s, pre_len);
   // (fused rank: K2 did not run; the flow count is this block's own)
   uint64_t fbase_f = 0;
   const uint64_t nflows = c.fused_rank ? fused_rank_block(c, s_map, fbase_f) : c.batch->flow_total;
@@ -1831,6 +1819,9 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   }
   const int mode = count_mode(c, nflows);
   if (blockIdx.x == 0 && tid == 0) c.persist_rw->k3_mode = (uint32_t)mode + 1u;
+  const uint64_t per = count_per(n_acc, gridDim.x);
+  const uint64_t lo = (uint64_t)blockIdx.x * per < n_acc ? (uint64_t)blockIdx.x * per : n_acc;
+  const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
   if (mode == 1) return;  // k_count_scatter
   if (mode == 3) {
     count_ranges<U, PACK>(c, n_acc, nflows, s_bin, s_map);
@@ -1858,14 +1849,8 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   for (uint64_t base = lo; base < hi; base += (uint64_t)UU * kCountBlock) {
     uint32_t s[UU], len[UU], id[UU];
     if (kK3LoadPrio) __builtin_amdgcn_s_setprio(kK3LoadPrio);
-    if constexpr (VEC) {
-      load_acc4<U>(c, base + 4ull * tid, hi, s, len);  // non-temporal
-    } else if (pre && base == lo) {
-#pragma unroll
-      for (int k = 0; k < U; ++k) s[k] = pre_s[k], len[k] = pre_len[k];
-    } else {
-      load_acc<U, PACK>(c, base + tid, lo, hi, s, len);  // streamed once: non-temporal
-    }
+    if constexpr (VEC) load_acc4<U>(c, base + 4ull * tid, hi, s, len);  // non-temporal
+    else load_acc<U, PACK>(c, base + tid, lo, hi, s, len);  // streamed once: non-temporal
     if (kK3LoadPrio) __builtin_amdgcn_s_setprio(0);
     if (ABL3 & 2) {
 #pragma unroll
