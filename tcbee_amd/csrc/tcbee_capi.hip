@@ -611,6 +611,7 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     if (!fuse) TRY_HIP(launch_rank(r, s));
     CountArgs k{};
     k.fused_rank = fuse ? 1u : 0u;
+    k.wide_iter = in->n >= kK3WideFrames ? 1u : 0u;
     k.new_list = c->d_new_list;
     k.batch_rw = c->d_batch;
     k.tab = c->tab;

@@ -195,6 +195,10 @@ struct CountArgs {
   // (mode 0 is certain), block 0 publishes cmap / cfs / flow_total and zeroes the new
   // ids' counters, and k_count_reduce advances the context's bases
   uint32_t fused_rank;
+  // k_count: 16 records per lane and iteration instead of 8 (batches of at least
+  // kK3WideFrames frames: twice the loads in flight; config 3, 100M records: K3
+  // -19..-34 us per step; 1M-record batches are slower with it)
+  uint32_t wide_iter;
   const uint64_t* new_list;  // (fused rank) slots first claimed this batch
   BatchState* batch_rw;      // (fused rank) the batch state K2 would have written
   FlowTable tab;             // (fused rank) slot fs32 words, cfs, cmap
@@ -210,6 +214,7 @@ struct CountArgs {
   PersistState* alt_persist;
 };
 constexpr uint64_t kFuseRankMax = 256;
+constexpr uint64_t kK3WideFrames = 16ull << 20;
 // g1 = k_count blocks; g1s = k_count_scatter blocks; g2 = k_count_bucket blocks
 // (g2 = 0: mode 1 impossible, neither is launched)
 hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned g2, hipStream_t s,

@@ -1783,7 +1783,8 @@ __device__ uint64_t fused_rank_block(const CountArgs& c, uint32_t* s_map, uint64
 }
 
 // ABL3 (timing-only ablations, 0 in every product launch): 1 no bin updates,
-// 2 no id gather, 4 no id stores.
+// 2 no id gather, 4 no id stores; 8 (A/B, variants build) plain id stores instead of
+// non-temporal ones.
 // Bins are indexed by CLAIM (dense in [0, F)); the record's output id is
 // omap[claim] (the local dense id, or — after a flow-hash exchange — the global
 // one), staged in LDS; k_count_reduce maps claims to local ids for the counters.
@@ -1885,7 +1886,10 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
 #pragma unroll
         for (int k = 0; k < U; ++k) {
           const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
-          if (p < hi && p < c.out_cap) __builtin_nontemporal_store(id[k], &c.out_id[p]);
+          if (p < hi && p < c.out_cap) {
+            if constexpr ((ABL3 & 8) != 0) c.out_id[p] = id[k];
+            else __builtin_nontemporal_store(id[k], &c.out_id[p]);
+          }
         }
       }
     }
@@ -3297,6 +3301,8 @@ static void launch_count_variant(const CountArgs& c, unsigned g1, unsigned g1s, 
     case 4: KC(8, 4); break;
     case 7: KC(8, 7); break;
     case 16: KC(16, 0); break;
+    case 8: KC(8, 8); break;    // plain id stores (A/B)
+    case 24: KC(16, 8); break;  // 16 records per lane, plain id stores (A/B)
     case 32: KC(4, 0); break;
     case 40:  // 16-B loads of four packed words per lane: U = 4 / 2 loads per lane
     case 42:  // (U = 8 spills 328 VGPRs)
@@ -3304,7 +3310,10 @@ static void launch_count_variant(const CountArgs& c, unsigned g1, unsigned g1s, 
       else if (c.pack_bits) hipLaunchKernelGGL((k_count<2, 0, true, true>), grid, dim3(kCountBlock), 0, s, c);
       else KC(8, 0);
       break;
-    default: KC(8, 0); break;
+    default:
+      if (c.wide_iter) KC(16, 0);
+      else KC(8, 0);
+      break;
   }
 #undef KC
   // the two-pass scatter only where the chunked one may not cover a batch (tables
@@ -3368,8 +3377,13 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
 #else
   (void)k3v;
   const dim3 grid(g1);
-  if (c.pack_bits) hipLaunchKernelGGL((k_count<8, 0, true>), grid, dim3(kCountBlock), 0, s, c);
-  else hipLaunchKernelGGL((k_count<8, 0, false>), grid, dim3(kCountBlock), 0, s, c);
+  if (c.wide_iter) {  // large batches: 16 records per lane and iteration
+    if (c.pack_bits) hipLaunchKernelGGL((k_count<16, 0, true>), grid, dim3(kCountBlock), 0, s, c);
+    else hipLaunchKernelGGL((k_count<16, 0, false>), grid, dim3(kCountBlock), 0, s, c);
+  } else {
+    if (c.pack_bits) hipLaunchKernelGGL((k_count<8, 0, true>), grid, dim3(kCountBlock), 0, s, c);
+    else hipLaunchKernelGGL((k_count<8, 0, false>), grid, dim3(kCountBlock), 0, s, c);
+  }
   // the two-pass scatter only where the chunked one may not cover a batch (tables
   // of >= kChunkMaxNb buckets): no empty launches otherwise
   const bool two_pass = !c.coffs || c.nb_max >= kChunkMaxNb;

@@ -513,15 +513,19 @@ def test_config4_1M_flows_device_right_sized(gpu, oracle, cap_mult):
         assert p.status() == 0
 
 
-@pytest.mark.parametrize("pool,n", [(10_500, 1_500_000), (17_000, 2_000_000),
-                                    (75_000, 2_500_000), (170_000, 3_000_000)])
-def test_k3_range_mode_large_batches(gpu, oracle, pool, n):
+@pytest.mark.parametrize("pool,n,k3v", [(10_500, 1_500_000, ""), (17_000, 2_000_000, ""),
+                                        (75_000, 2_500_000, ""), (170_000, 3_000_000, ""),
+                                        (10_500, 1_500_000, "16"), (17_000, 2_000_000, "16")])
+def test_k3_range_mode_large_batches(gpu, oracle, pool, n, k3v, monkeypatch):
     """Large-table K3 on one batch, device-resident: mode 3 at 2 and 3 claim ranges,
     mode 1 beyond (143k flows: 36 buckets, lane-scattered; ~290k flows: 71 buckets,
     the LDS-staged scatter); a mixed trace with hot, rejected and > 64 KiB frames;
-    ids, the whole table and counters vs the oracle."""
+    ids, the whole table and counters vs the oracle. k3v "16": the variants build
+    with 16 records per lane and iteration (what the product runs on batches of
+    >= 16M frames), mode 3 here."""
     import torch
     from tracegen import mixed_trace
+    monkeypatch.setenv("TCBEE_K3ABL", k3v or "0")
     tr = mixed_trace(n, seed=pool, n_flows=pool)  # ~1.9 distinct keys per pool flow
     ln = tr.caplen.copy()
     rng = np.random.default_rng(7)
@@ -538,7 +542,7 @@ def test_k3_range_mode_large_batches(gpu, oracle, pool, n):
     fi_d = torch.empty(n, dtype=torch.int32, device="cuda")
     n_d = torch.zeros(1, dtype=torch.int64, device="cuda")
     ctr_d = torch.zeros(4, dtype=torch.int64, device="cuda")
-    with tcbee_amd.PacketParser(max_frames=n, max_flows=4 * pool) as p:
+    with tcbee_amd.PacketParser(max_frames=n, max_flows=4 * pool, variants=bool(k3v)) as p:
         s = torch.cuda.current_stream().cuda_stream
         p.parse_device(d_arena, len(tr.arena), d_off, d_len, d_ts, n, rec_d, n, None, fi_d, n_d,
                        ctr_d, stream=s)
@@ -794,11 +798,12 @@ def test_max_wide_flows_exact_bound(gpu, oracle, short):
         assert not np.isin(fi[~refused], keys).any()
 
 
-@pytest.mark.parametrize("k3v", ["40", "42"])
+@pytest.mark.parametrize("k3v", ["40", "42", "16"])
 @pytest.mark.parametrize("flows", [1, 40, 5000])
 def test_k3_vector_loads_variant(gpu, oracle, flows, k3v, monkeypatch):
     """K3 mode 0 with 16-B loads of four packed K1 -> K3 words per lane (variants
-    build, TCBEE_K3ABL=40/42: 4 / 2 loads per lane): a ragged tail (scalar fallback),
+    build, TCBEE_K3ABL=40/42: 4 / 2 loads per lane), and with 16 records per lane and
+    iteration (16: the product's form for batches of >= 16M frames): a ragged tail (scalar fallback),
     saturated packed caplens (the side array), > 64 KiB frames (device atomics), a
     hot flow (the wave-uniform add) — bit-exact vs the oracle."""
     from tracegen import mixed_trace
