@@ -865,3 +865,15 @@ def test_small_context_generations_and_prep_free_batches(gpu, oracle):
                 assert p.status() == 0
         finally:
             oracle.free_flowtab(ft)
+
+
+def test_k3_wide_iteration_large_batch(gpu, oracle):
+    """Batches of >= 16M frames run K3 with 16 records per lane and iteration
+    (CountArgs::wide_iter, the product's config-3 form): 16.8M 64-B frames over 3000
+    flows, a ragged last block — records, hashes, ids, counters and the table vs the
+    oracle, count mode 0."""
+    n = (16 << 20) + 12_345
+    tr = tcbee_amd.synth_trace(n, sizes="64", kind=1, n_flows=3000)
+    with tcbee_amd.PacketParser(max_frames=n, max_arena=len(tr.arena), max_flows=4096) as p:
+        assert_same(p.parse(tr), oracle.parse(tr), p.flows())
+        assert p.status() == 0 and p.count_mode() == 0
