@@ -877,3 +877,68 @@ def test_k3_wide_iteration_large_batch(gpu, oracle):
     with tcbee_amd.PacketParser(max_frames=n, max_arena=len(tr.arena), max_flows=4096) as p:
         assert_same(p.parse(tr), oracle.parse(tr), p.flows())
         assert p.status() == 0 and p.count_mode() == 0
+
+
+def _fuzz_trace(seed: int, n: int, pool: int, port: int) -> Trace:
+    """Random frames in a random-byte arena: caplens around every accept boundary
+    (< 14, 53/54, 73/74) and up to 70 000 B (such a frame runs over the next ones),
+    ethertype IPv4 / IPv6 / other, protocol TCP or not; with `pool` > 0 the addresses
+    and ports come from `pool` keys (one of them carrying `port`), else they stay
+    random. Frame starts are >= 64 B apart (no frame's header bytes are another's)."""
+    rng = np.random.default_rng(seed)
+    edge = np.array([0, 1, 13, 14, 15, 33, 53, 54, 55, 72, 73, 74, 75, 76, 96, 70_000])
+    ln = np.where(rng.random(n) < 0.3, edge[rng.integers(0, len(edge), n)],
+                  rng.integers(0, 400, n))
+    stride = np.maximum(np.minimum(ln, 400), 64) + rng.integers(0, 16, n)
+    off = np.concatenate([[0], np.cumsum(stride[:-1])]).astype(np.int64)
+    arena = rng.integers(0, 256, size=int(off[-1]) + 70_000 + 64, dtype=np.uint8)
+    et = rng.choice([0x0800, 0x86DD, 0x8100, 0x0806], size=n, p=[0.45, 0.4, 0.1, 0.05])
+    arena[off + 12] = et >> 8
+    arena[off + 13] = et & 0xFF
+    v4 = et == 0x0800
+    tcp = rng.random(n) < 0.85
+    arena[np.where(v4, off + 23, off + 20)] = np.where(tcp, 6, rng.integers(0, 256, n))
+    if pool:
+        # key bytes: 32 address bytes (v4 uses the first 8) + sport, dport
+        key = rng.integers(0, 256, size=(pool, 36), dtype=np.uint8)
+        key[0, 34:36] = [port >> 8, port & 0xFF]
+        k = rng.integers(0, pool, n)
+        i4, i6 = np.nonzero(v4)[0], np.nonzero(~v4)[0]
+        for j in range(8):  # v4: saddr, daddr at 26..33, ports at 34..37
+            arena[off[i4] + 26 + j] = key[k[i4], j]
+        for j in range(32):  # v6: saddr, daddr at 22..53, ports at 54..57
+            arena[off[i6] + 22 + j] = key[k[i6], j]
+        for j in range(4):
+            arena[off[i4] + 34 + j] = key[k[i4], 32 + j]
+            arena[off[i6] + 54 + j] = key[k[i6], 32 + j]
+    ts = rng.integers(0, 2**63, size=n, dtype=np.int64).astype(np.uint64)
+    return Trace(arena, off.astype(np.uint64), ln.astype(np.uint32), ts)
+
+
+@pytest.mark.parametrize("seed,pool,port", [(1, 0, 0), (2, 40, 0), (3, 40, 4242), (4, 3000, 0)])
+def test_random_frames_fuzz(gpu, oracle, seed, pool, port):
+    """Random frames (_fuzz_trace) through one batch and through three batches of a
+    kept table: records, hashes, ids, counters and the table bit-exact vs the oracle
+    (pool 40: a small context — two table generations, the fused rank; pool 0: a
+    distinct key per accepted frame)."""
+    n = 300_000
+    tr = _fuzz_trace(seed, n, pool, port)
+    orc = oracle.parse(tr, filter_port=port)
+    nf = max(len(orc[4]), 16)
+    cap = 256 if pool == 40 else nf + 64
+    with tcbee_amd.PacketParser(max_frames=n, max_arena=len(tr.arena), max_flows=cap) as p:
+        assert_same(p.parse(tr, filter_port=port), orc, p.flows())
+        assert p.status() == 0
+        p.reset_flows()
+        ft = oracle.new_flowtab(1 << 20)
+        base = 0
+        try:
+            for lo, hi in [(0, 1000), (1000, 123_457), (123_457, n)]:
+                part = tr.select(np.arange(lo, hi))
+                o = oracle.parse(part, ft=ft, record_base=base, filter_port=port)
+                assert_same(p.parse(part, filter_port=port), o)
+                base += len(o[0])
+            assert np.array_equal(p.flows(), oracle.flows(ft))
+        finally:
+            oracle.free_flowtab(ft)
+        assert p.status() == 0
