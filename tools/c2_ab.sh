@@ -1,6 +1,6 @@
 #!/bin/bash
 # Config 2 (1M x 64 B, one flow, reset per step) under several libraries, alternating
-# processes: NAMES="HEAD wt_t8 ..." (build/ab_<name>/libtcbee_amd.so, tools/lib_ab.sh
+# processes: NAMES="HEAD wt_x ..." (build/ab_<name>/libtcbee_amd.so, tools/lib_ab.sh
 # build), PAIRS rounds. Each process: tools/c2_warm.py (bench.py's own run_device).
 set -u
 mkdir -p gpurun_out
