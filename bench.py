@@ -65,6 +65,9 @@ def build_device_trace(torch, n, sizes, kind, n_flows, seed, first_index, stream
 RSS_WINDOW = 16_000_000  # frames of observed traffic an RSS table is balanced on
 
 
+RSS_SKEW_LIMIT = 1.25  # max / mean flows per rank a flow-hash run accepts (before timing)
+
+
 def rss_for(torch, n_global, world, kind, n_flows, seed, stream):
     """The NIC's RSS indirection table (4096 hash buckets -> GPUs) balanced on the
     bucket loads of RSS_WINDOW frames of the same synthetic stream OUTSIDE the
@@ -72,26 +75,48 @@ def rss_for(torch, n_global, world, kind, n_flows, seed, stream):
     receive-side scaling is rebalanced from earlier load — ADVICE r3: balancing on
     the measured frames made the imbalance in-sample), via
     tcbee_gen_rss_load_range_device and tcbee_amd.rss_table; the same table on every
-    rank. Every flow still lands on one GPU. Returns the table on the device and what
-    the line reports (TCBEE_BENCH_RSS=0: None, the modulo placement
-    fold32(hash) % world); the measured imbalance is the line's shard_imbalance."""
+    rank. Every flow still lands on one GPU. Returns the table on the device (None:
+    the modulo placement fold32(hash) % world; TCBEE_BENCH_RSS=0), what the line
+    reports, and the flows each rank will hold (tcbee_amd.rss_flows_per_rank: the
+    flows routed to it, known before any frame is parsed), from which the table and
+    exchange capacities are sized. A partition whose busiest rank holds more than
+    RSS_SKEW_LIMIT x the mean flows is refused HERE, before anything is timed, on
+    every rank alike (the same table everywhere: no rank waits in a collective).
+    TCBEE_BENCH_RSS=skew (test hook): every bucket but one on rank 0."""
     import tcbee_amd
-    if world < 2 or os.environ.get("TCBEE_BENCH_RSS", "1") == "0":
-        return None, {"rss": None}
-    win = RSS_WINDOW
-    counts = torch.empty(tcbee_amd.RSS_BUCKETS, dtype=torch.int64, device="cuda")
-    tcbee_amd.gen_rss_load_device(win, kind, n_flows, seed, counts, stream=stream,
-                                  first_frame=n_global)
-    load = counts.cpu().numpy()
-    table = tcbee_amd.rss_table(load, world)
-    per = np.bincount(table, weights=load, minlength=world)
-    info = {"rss": {"buckets": len(table), "balanced_on_frames": [n_global, n_global + win],
-                    "held_out": True,
-                    "window_imbalance": round(float(per.max() / per.mean()), 5)}}
-    if len(table) % world == 0:  # the modulo placement on the same window, for reference
-        mod = np.bincount(np.arange(len(table)) % world, weights=load, minlength=world)
-        info["rss"]["window_imbalance_modulo"] = round(float(mod.max() / mod.mean()), 5)
-    return torch.from_numpy(table.view(np.int16)).cuda(), info
+    mode = os.environ.get("TCBEE_BENCH_RSS", "1")
+    table = None
+    info = {"rss": None}
+    if world >= 2 and mode == "skew":
+        table = np.zeros(tcbee_amd.RSS_BUCKETS, dtype=np.uint16)
+        table[1:world] = np.arange(1, world, dtype=np.uint16)
+        info = {"rss": {"buckets": len(table), "skewed_test_table": True}}
+    elif world >= 2 and mode != "0":
+        win = RSS_WINDOW
+        counts = torch.empty(tcbee_amd.RSS_BUCKETS, dtype=torch.int64, device="cuda")
+        tcbee_amd.gen_rss_load_device(win, kind, n_flows, seed, counts, stream=stream,
+                                      first_frame=n_global)
+        load = counts.cpu().numpy()
+        table = tcbee_amd.rss_table(load, world)
+        per = np.bincount(table, weights=load, minlength=world)
+        info = {"rss": {"buckets": len(table), "balanced_on_frames": [n_global, n_global + win],
+                        "held_out": True,
+                        "window_imbalance": round(float(per.max() / per.mean()), 5)}}
+        if len(table) % world == 0:  # the modulo placement on the same window, for reference
+            mod = np.bincount(np.arange(len(table)) % world, weights=load, minlength=world)
+            info["rss"]["window_imbalance_modulo"] = round(float(mod.max() / mod.mean()), 5)
+    flows_per_rank = (tcbee_amd.rss_flows_per_rank(n_flows, world, seed, table)
+                      if kind == 1 else np.full(world, n_flows if world == 1 else 1, np.int64))
+    skew = float(flows_per_rank.max() / max(flows_per_rank.mean(), 1e-9))
+    if world >= 2 and kind == 1:
+        info["flows_per_rank"] = [int(flows_per_rank.min()), int(flows_per_rank.max())]
+        if skew > RSS_SKEW_LIMIT:
+            raise RuntimeError(
+                f"flow-hash partition refused before the timed region: its busiest rank "
+                f"holds {int(flows_per_rank.max())} of {n_flows} flows, {skew:.2f}x the mean "
+                f"(limit {RSS_SKEW_LIMIT}); rebalance the RSS table")
+    dev = torch.from_numpy(table.view(np.int16)).cuda() if table is not None else None
+    return dev, info, flows_per_rank
 
 
 def build_shard_trace(torch, n_global, world, rank, sizes, kind, n_flows, seed, stream,
@@ -154,7 +179,7 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     if flowhash:
         # n frames per GPU on average: rank `rank` parses the frames of ITS flows out of
         # a global trace of n * world frames (sizes differ by a few hundred)
-        rss, rss_info = rss_for(torch, n_global, sw, kind, n_flows, seed, stream)
+        rss, rss_info, flows_per_rank = rss_for(torch, n_global, sw, kind, n_flows, seed, stream)
         d_arena, alen, d_off, d_len, d_ts, gidx, n = build_shard_trace(
             torch, n_global, sw, rank, sizes, kind, n_flows, seed, stream, rss=rss)
         first = 0
@@ -188,21 +213,24 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
               "id": torch.empty(n, dtype=torch.int32, device="cuda"),
               "n": torch.zeros(1, dtype=torch.int64, device="cuda"),
               "ctr": torch.zeros(4, dtype=torch.int64, device="cuda")} for _ in range(nbuf)]
-    # flow-hash shards hold ~n_flows/world flows each; the exchange carries `xcap`
-    # entries per rank (checked against the real count after the run)
-    flows_here = -(-n_flows // sw) if flowhash else n_flows
+    # flow-hash shards: the flows routed to each rank are known before any frame is
+    # parsed (rss_for); the exchange carries `xcap` entries per rank, sized for the
+    # busiest rank (every rank's all-gather block has the same size)
+    flows_here = int(flows_per_rank[rank]) if flowhash else n_flows
     # table: max_flows = the shard's expected flows + 3 % + 64 (a flow-hash shard of
     # config 3 at N=8 holds up to +3 % of the mean; claims past max_flows are
     # refused). The compact table (round 3) keeps 8 slots per max_flow (load <=
     # 1/8), 6 slots per 128-B line: 176 MB at 1M flows (rounds 1-2: 64-B slots at
     # max_flows = 4x flows, 512 MiB), and a tight max_flows keeps the K1 -> K3 word
     # packed (claim | caplen) up to 2^20 flows
-    # (+4 sigma of a binomial shard size on top, so no seed's RSS spread can refuse
-    # a flow; 1M flows stay below 2^20 + ... = packed K1 -> K3 words)
-    cap = max(flows_here + int(4 * flows_here ** 0.5) + flows_here // 32 + 64, 64)
-    # (the exchange carries up to xcap entries per rank: a quarter more than the
-    # shard's expected flows)
-    xcap = max(int(1.25 * flows_here) + 4096, 1 << 12)
+    # (flow-hash shards: flows_here is exact, an upper bound the shard reaches once
+    # every one of its flows has appeared; 1M flows stay below 2^20 = packed K1 -> K3
+    # words)
+    cap = max(flows_here + flows_here // 32 + 64, 64)
+    # (the exchange carries up to xcap entries per rank: the busiest rank's flows, or a
+    # quarter more than a contiguous shard's)
+    xcap = (int(flows_per_rank.max()) + 64 if flowhash
+            else max(int(1.25 * flows_here) + 4096, 1 << 12))
     p = tcbee_amd.PacketParser(device=torch.cuda.current_device(), max_frames=n, max_arena=0,
                                max_flows=cap)
     merged = om = fm = fx = ox = None

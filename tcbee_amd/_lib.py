@@ -221,6 +221,9 @@ def lib(variants: bool = False) -> C.CDLL:
         _share_hip_runtime_with_torch()
         L = C.CDLL(path)
         for name, (res, args) in _SIGS.items():
+            # (an older build under TCBEE_AB_LIB may predate some entry points)
+            if os.environ.get("TCBEE_AB_LIB") and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -843,7 +843,11 @@ void k_parse(ParseArgs a) {
         if (v4k[f]) {
           S0[f] = home_slot(h[f], a.tab.nlines);
           uint32_t l = slot_line(S0[f]), pos = S0[f] - l * kSlotsPerLine;
-          if (ABL & 64) l = (uint32_t)(h[f] >> 40) & ((16u << 20) / 64u - 1u);
+          // probe window of the ceiling ablation: 64 = 16 MiB (Infinity-Cache resident),
+          // +128 = 2 MiB, +256 = 4 MiB, +384 = 512 KiB (L2-sized first levels)
+          constexpr uint32_t kAblWin = (ABL & 384) == 128 ? (2u << 20) : (ABL & 384) == 256 ? (4u << 20)
+                                     : (ABL & 384) == 384 ? (512u << 10) : (16u << 20);
+          if (ABL & 64) l = (uint32_t)(h[f] >> 40) & (kAblWin / 64u - 1u);
           Q[f][0] = __builtin_amdgcn_raw_buffer_load_b128(sl_rs, l * 64u + 16u * pos, 0, PROBE_AUX);
           // (the slot and its fs32 share one 64-B half-line: the two halves of a
           //  128-B line can be of different ages in L1/L2 — a fresh published slot
@@ -2195,7 +2199,9 @@ __global__ __launch_bounds__(BS) void k_count_chunk(CountArgs c) {
 // the region entry at region[chunk + idx] and the id back into s_rw[pos] — a slot
 // only its own reader touches, so no barrier between the gather and the write-back.
 constexpr uint32_t kLenSat = 2047;  // caplens >= kLenSat are re-read from the K1 scratch
-template <bool PACK, int BS, int U, int WG_PER_CU = 2>
+// CABL (timing-only ablations, variants build; 0 in product launches): 1 no claim -> id
+// gather (id = claim), 2 no region stores, 4 no id stores
+template <bool PACK, int BS, int U, int WG_PER_CU = 2, int CABL = 0>
 // (WG_PER_CU workgroups of BS / 64 waves on a CU's 4 SIMDs)
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WG_PER_CU * BS / 256, 8)))
 void k_count_chunk2(CountArgs c) {
@@ -2316,13 +2322,14 @@ void k_count_chunk2(CountArgs c) {
             l = al[pos];
           }
         }
-        rg[idx] = (cl & (kBucket - 1u)) | l << kBucketBits;  // coalesced runs
-        id = c.omap[cl];  // one bucket's 16 KiB window per wave: L1-local
+        if (!(CABL & 2)) rg[idx] = (cl & (kBucket - 1u)) | l << kBucketBits;  // coalesced runs
+        else asm volatile("" ::"v"(l));
+        id = (CABL & 1) ? cl : c.omap[cl];  // one bucket's 16 KiB window per wave: L1-local
       }
       s_rw[pos] = id;  // only this thread reads or writes slot pos in this phase
     }
     __syncthreads();
-    if (c.out_id && base < c.out_cap) {
+    if (c.out_id && base < c.out_cap && !(CABL & 4)) {
       uint32_t* oi = c.out_id + base;
       const uint32_t lim = c.out_cap - base < nval ? (uint32_t)(c.out_cap - base) : nval;
 #pragma unroll
@@ -3208,6 +3215,7 @@ static bool launch_parse_variant(const ParseArgs& a, bool flows, hipStream_t s, 
     switch (abl) {
       TCBEE_ABL_CASE(1) TCBEE_ABL_CASE(2) TCBEE_ABL_CASE(4) TCBEE_ABL_CASE(8)
       TCBEE_ABL_CASE(16) TCBEE_ABL_CASE(3) TCBEE_ABL_CASE(31) TCBEE_ABL_CASE(32) TCBEE_ABL_CASE(96)
+      TCBEE_ABL_CASE(224) TCBEE_ABL_CASE(352) TCBEE_ABL_CASE(480)
       default: break;
     }
 #undef TCBEE_ABL_CASE
@@ -3350,6 +3358,14 @@ static void launch_count_variant(const CountArgs& c, unsigned g1, unsigned g1s, 
       if (k3v == 94) {
         if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk2<true, 1024, 12>), gc, dim3(1024), 0, s, c);
         else hipLaunchKernelGGL((k_count_chunk2<false, 1024, 12>), gc, dim3(1024), 0, s, c);
+      } else if (k3v >= 101 && k3v <= 107 && c.pack_bits) {  // 100 + CABL: timing-only ablations
+#define TCBEE_CABL_CASE(A) \
+        case 100 + A: hipLaunchKernelGGL((k_count_chunk2<true, 512, 24, 2, A>), gc, dim3(512), 0, s, c); break;
+        switch (k3v) {
+          TCBEE_CABL_CASE(1) TCBEE_CABL_CASE(2) TCBEE_CABL_CASE(3) TCBEE_CABL_CASE(4) TCBEE_CABL_CASE(5)
+          TCBEE_CABL_CASE(6) TCBEE_CABL_CASE(7)
+        }
+#undef TCBEE_CABL_CASE
       } else {
         if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk2<true, 512, 24>), gc, dim3(512), 0, s, c);
         else hipLaunchKernelGGL((k_count_chunk2<false, 512, 24>), gc, dim3(512), 0, s, c);

@@ -63,10 +63,15 @@ class PacketParser:
         self._L = L
         h = C.c_void_p()
         wide = max_flows if max_wide_flows is None else max_wide_flows
-        _lib.check(L.tcbee_ctx_create_ex(C.byref(h), device, C.c_uint64(max_frames),
-                                         C.c_uint64(max_arena), C.c_uint64(max_flows),
-                                         C.c_uint64(wide)),
-                   "tcbee_ctx_create_ex")
+        if hasattr(L, "tcbee_ctx_create_ex"):
+            _lib.check(L.tcbee_ctx_create_ex(C.byref(h), device, C.c_uint64(max_frames),
+                                             C.c_uint64(max_arena), C.c_uint64(max_flows),
+                                             C.c_uint64(wide)),
+                       "tcbee_ctx_create_ex")
+        else:  # an ABI-4 library under TCBEE_AB_LIB (A/B tooling only)
+            _lib.check(L.tcbee_ctx_create(C.byref(h), device, C.c_uint64(max_frames),
+                                          C.c_uint64(max_arena), C.c_uint64(max_flows)),
+                       "tcbee_ctx_create")
         self._h = h
         self._owned = True
         self.device = device

@@ -196,3 +196,59 @@ def rss_table(load, world: int) -> np.ndarray:
         heapq.heappush(heap, (tot[g], g))
     return table
 
+
+
+def flow_hash64_np(k0, k1, k2, k3, k4) -> np.ndarray:
+    """Vectorised flow hash v1 (== tcbee::flow_hash64 in tcbee_layout.h) of keys given
+    as five LE u64 word arrays."""
+    c1, c2 = np.uint64(0x87C37B91114253D5), np.uint64(0x4CF5AD432745937F)
+    s31, s33 = np.uint64(31), np.uint64(33)
+    h = np.full(np.shape(k0), 0x7CBEE, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        for k in (k0, k1, k2, k3, k4):
+            h ^= np.asarray(k, dtype=np.uint64) * c1
+            h = ((h << s31) | (h >> s33)) * c2
+        h ^= np.uint64(40)
+        h ^= h >> s33
+        h *= np.uint64(0xFF51AFD7ED558CCD)
+        h ^= h >> s33
+        h *= np.uint64(0xC4CEB9FE1A85EC53)
+        h ^= h >> s33
+    return h
+
+
+def synth_flow_folds(n_flows: int, seed: int = DEFAULT_SEED) -> np.ndarray:
+    """fold32(flow_hash64(IpTuple)) of every flow f < n_flows of the multi-flow
+    synthetic trace (tcbee_gen.h gen_fields: the flow's addresses and ports from
+    splitmix64((seed << 1) ^ (0xF10F10000000 + f)); the key K1 builds, xdp.rs:116-127)
+    — the value a NIC's RSS (and the device shard generator, gen_fold) buckets a
+    flow's frames by. uint32[n_flows]."""
+    f = np.arange(n_flows, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        fh = splitmix64(np.uint64((seed << 1) & 0xFFFFFFFFFFFFFFFF) ^ (np.uint64(0xF10F10000000) + f))
+    m24, m20 = np.uint64(0xFFFFFF), np.uint64(0xFFFFF)
+    saddr = (np.uint64(0x0A000000) | (fh & m24)).astype(np.uint32)
+    daddr = (np.uint64(0xAC100000) | ((fh >> np.uint64(24)) & m20)).astype(np.uint32)
+    sport = np.uint64(1024) + (fh >> np.uint64(44)) % np.uint64(64000)
+    dport = np.array([80, 443, 5201, 8080], dtype=np.uint64)[(fh >> np.uint64(62)).astype(np.int64)]
+    k1 = saddr.byteswap().astype(np.uint64) << np.uint64(32)
+    k3 = daddr.byteswap().astype(np.uint64) << np.uint64(32)
+    k4 = sport | (dport << np.uint64(16)) | (np.uint64(6) << np.uint64(32))
+    zero = np.zeros(n_flows, dtype=np.uint64)
+    h = flow_hash64_np(zero, k1, zero, k3, k4)
+    return (h ^ (h >> np.uint64(32))).astype(np.uint32)
+
+
+def rss_flows_per_rank(n_flows: int, world: int, seed: int = DEFAULT_SEED,
+                       table: np.ndarray | None = None) -> np.ndarray:
+    """Flows each rank of a flow-hash partition holds at most (exactly, once every
+    flow has appeared): flows f < n_flows routed through the RSS indirection table
+    (bucket fold32 % len(table)) or, without one, the modulo placement fold32 % world.
+    Known before any frame is parsed, so shard capacities come from it. int64[world]."""
+    folds = synth_flow_folds(n_flows, seed)
+    if table is None:
+        owner = folds % np.uint32(world)
+    else:
+        t = np.asarray(table)
+        owner = t[(folds % np.uint32(len(t))).astype(np.int64)]
+    return np.bincount(owner.astype(np.int64), minlength=world).astype(np.int64)

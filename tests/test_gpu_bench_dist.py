@@ -30,13 +30,17 @@ def free_port() -> int:
     return port
 
 
-def run_bench_world(world: int, args: list[str], timeout: int = 420) -> dict:
-    env = dict(os.environ, TCBEE_DIST_BACKEND="gloo", PYTHONUNBUFFERED="1")
+def launch(world: int, args: list[str], timeout: int, **env_extra):
+    env = dict(os.environ, TCBEE_DIST_BACKEND="gloo", PYTHONUNBUFFERED="1", **env_extra)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
            "--master-port", str(free_port()), "bench.py", "--gpus", str(world)] + args
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True,
-                       timeout=timeout)
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True,
+                          timeout=timeout)
+
+
+def run_bench_world(world: int, args: list[str], timeout: int = 420) -> dict:
+    r = launch(world, args, timeout)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints ONE line
@@ -71,3 +75,38 @@ def test_bench_world2_flowhash_and_config4_leg(gpu):
     # 12M IMIX frames of 1M uniform flows: almost every flow appears
     assert 990_000 < c4["check"]["flows"] <= 1_000_000
     assert c4["check"]["pkts_total"] == 12_000_000
+
+
+def test_bench_world4_flowhash_and_config4_leg(gpu):
+    """World 4 (four ranks on device 0 over gloo): both legs bit-exact on every rank,
+    the exchange capacity sized from the RSS table's flows per rank."""
+    out = run_bench_world(4, ["--frames", "2000000", "--steps", "2", "--warmup", "1",
+                              "--c4-frames", "3000000", "--c4-steps", "2", "--no-cpu"],
+                          timeout=600)
+    assert out["n_gpus"] == 4 and out["dist"] == {"backend": "gloo", "world_size": 4}
+    chk = out["check"]
+    check_leg(chk, 4)
+    assert chk["flows"] == 10_000 and chk["pkts_total"] == 4 * 2_000_000
+    lo, hi = chk["flows_per_rank"]
+    assert 0 < lo <= hi < 1.1 * 10_000 / 4
+    c4 = out["config4_flowhash"]
+    assert c4["frames_global"] == 12_000_000 and c4["flows"] == 1_000_000
+    check_leg(c4["check"], 4)
+    assert c4["check"]["pkts_total"] == 12_000_000
+    lo4, hi4 = c4["check"]["flows_per_rank"]
+    assert 240_000 < lo4 <= hi4 < 260_000
+
+
+def test_bench_skewed_rss_refused_before_timing(gpu):
+    """A deliberately skewed RSS table (every bucket but a few on rank 0) is refused
+    while the shards are being sized — before any step is timed — with a clear
+    message on every rank, instead of overflowing the exchange after the run."""
+    import time
+    t0 = time.perf_counter()
+    r = launch(2, ["--frames", "2000000", "--steps", "2", "--warmup", "1", "--no-cpu",
+                   "--no-extra"], timeout=300, TCBEE_BENCH_RSS="skew")
+    assert r.returncode != 0
+    assert "refused before the timed region" in r.stderr
+    assert "steps in" not in r.stderr  # bench.run_device's "N steps in X ms" never logged
+    assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert time.perf_counter() - t0 < 240

@@ -74,6 +74,8 @@ def main():
         for r in range(args.rounds):
             for v in variants:
                 p = parsers[v]
+                if var_name:  # (the variants build reads TCBEE_ABLATE & co at every launch)
+                    os.environ[var_name] = v[2]
                 def step():
                     if not args.warm:
                         p.reset_flows(stream=stream, sync=False)  # one fresh trace per step, as bench.py
