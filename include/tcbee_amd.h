@@ -144,6 +144,12 @@ int         tcbee_device_count(int* n);
  *             slots of 64 B (512-1024 B per wide flow: 512 MiB at 1M), allocated
  *             whatever the trace holds; tcbee_ctx_create sizes them for
  *             max_wide_flows = max_flows.
+ *             Per frame of max_frames: 8 B of K1 -> K3 words (+8 B for a second
+ *             slot once an asynchronous-ids batch runs), a first-seen bit, and for
+ *             tables of more than 12288 flows ~4.2 B of K3 mode-1 scratch. A small
+ *             context (max_flows <= 256) with max_frames <= 2^20 also keeps a
+ *             second table generation and the second slot from creation (8 B per
+ *             frame + ~88 KB), so that a table reset costs no launch.
  * device    : HIP device ordinal. */
 int tcbee_ctx_create(tcbee_ctx** out, int device, uint64_t max_frames,
                      uint64_t max_arena, uint64_t max_flows);
@@ -499,7 +505,9 @@ int tcbee_pipe_run(tcbee_pipe* p, const tcbee_frames* in_host, const tcbee_cfg* 
  * out_cap still goes through staging. The sink then receives pointers into the
  * caller's arrays. out_flow_id may be NULL (records only). Registering another
  * pair (or NULL, 0, NULL) releases the previous one; tcbee_pipe_destroy releases
- * it too. The caller keeps the arrays alive while registered. */
+ * it too. The caller keeps the arrays alive while registered. An array already
+ * page-locked (by another pipe, or by the caller's hipHostRegister) is used as it
+ * is and left page-locked on release, so several pipes may share one pair. */
 int tcbee_pipe_register_output(tcbee_pipe* p, uint8_t* out_rec74, uint64_t cap,
                                uint32_t* out_flow_id);
 

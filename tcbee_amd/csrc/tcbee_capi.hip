@@ -23,11 +23,14 @@ struct tcbee_ctx {
   bool reset_pending = false;   // tcbee_flow_reset_device: applied by the next launch
   uint32_t withhold_every = 0;  // TCBEE_TEST_WITHHOLD (look-back recount test hook)
   int k3_no_bucket = 0;         // TCBEE_TEST_K3_NOBUCKET=1: large tables use K3 mode 2 (test hook)
-  int k3_variant = 0;           // TCBEE_K3ABL: timing-only K3 ablations / tilings (A/B)
+  bool k3_twopass = false;      // TCBEE_TEST_K3_TWOPASS=1: mode 1 by the two-pass scatter
+                                // at any bucket count (test hook; the product takes it
+                                // only past kChunkMaxNb buckets)
+  bool k3_wide = false;         // TCBEE_TEST_K3_WIDE=1: 16 records per lane in k_count on
+                                // every batch (test hook; the product: >= kK3WideFrames)
   bool k3_range = false;        // K3 mode 3 available (part rows sized for it)
-  int k1_variant = 0;           // TCBEE_K1V: K1 staging/occupancy A/B variants
-  uint32_t async_k3_blocks = 0; // TCBEE_ASYNC_K3_BLOCKS: K3 grid cap with async ids (A/B)
-  uint32_t plain_walk = kPlainWalk;  // TCBEE_WALK: K1 plain probe walk length (A/B)
+  uint32_t plain_walk = kPlainWalk;  // TCBEE_WALK: K1 plain probe walk length (test hook:
+                                     // 0 sends every foreign slot to the coherent path)
   bool no_fuse_rank = false;         // TCBEE_NO_FUSE_RANK: the separate rank launch (A/B, tests)
   uint32_t pack_bits = 0;            // K1->K3 scratch packing (0: two words per record)
 
@@ -69,7 +72,7 @@ struct tcbee_ctx {
   uint32_t* d_k3_region = nullptr;   // K3 mode 1 (tables with > kCountBins slots only)
   uint32_t* d_k3_offs = nullptr;
   uint64_t* d_k3_lpart = nullptr;
-  uint32_t* d_k3_coffs = nullptr;    // k_count_chunk: bucket offsets per kChunk records
+  uint32_t* d_k3_coffs = nullptr;    // k_count_chunk2: bucket offsets per kChunk records
   uint32_t k3_nb_max = 0, k3_g2 = 0;
   uint64_t k3_g1max = 0, part_words = 0;
   int n_cu = 256;
@@ -133,9 +136,7 @@ void dfree(void* p) {
   if (p) (void)hipFree(p);
 }
 
-uint64_t tile_frames(int fpl, int k1v = 0) {
-  return (uint64_t)kBlock * (uint64_t)fpl * (k1v == 20 ? 2u : 1u);  // 20: 512-thread tiles
-}
+uint64_t tile_frames(int fpl) { return (uint64_t)kBlock * (uint64_t)fpl; }
 
 int ensure_host_path(tcbee_ctx* c) {
   if (c->d_arena) return TCBEE_OK;
@@ -286,9 +287,8 @@ int tcbee_ctx_create_ex(tcbee_ctx** out, int device, uint64_t max_frames, uint64
   // library reads no environment variable
   if (const char* e = std::getenv("TCBEE_TEST_WITHHOLD")) c->withhold_every = (uint32_t)std::atoi(e);
   if (const char* e = std::getenv("TCBEE_TEST_K3_NOBUCKET")) c->k3_no_bucket = std::atoi(e);
-  if (const char* e = std::getenv("TCBEE_K3ABL")) c->k3_variant = std::atoi(e);
-  if (const char* e = std::getenv("TCBEE_K1V")) c->k1_variant = std::atoi(e);
-  if (const char* e = std::getenv("TCBEE_ASYNC_K3_BLOCKS")) c->async_k3_blocks = (uint32_t)std::atoi(e);
+  if (const char* e = std::getenv("TCBEE_TEST_K3_TWOPASS")) c->k3_twopass = std::atoi(e) != 0;
+  if (const char* e = std::getenv("TCBEE_TEST_K3_WIDE")) c->k3_wide = std::atoi(e) != 0;
   if (const char* e = std::getenv("TCBEE_WALK")) c->plain_walk = (uint32_t)std::atoi(e);
   if (const char* e = std::getenv("TCBEE_NO_FUSE_RANK")) c->no_fuse_rank = std::atoi(e) != 0;
   if (const char* e = std::getenv("TCBEE_FPL")) {
@@ -399,15 +399,18 @@ int tcbee_ctx_create_ex(tcbee_ctx** out, int device, uint64_t max_frames, uint64
       return fail(map_err(e));
     if ((e = dalloc(&c->d_k3_lpart, 2ull * c->k3_g2 * kBucket)) != hipSuccess)
       return fail(map_err(e));
-    // single-pass chunked scatter (batches of <= kSmallNb buckets): offsets of every
-    // chunk's buckets (4 B x 513 per 16384 frames)
-    if ((e = dalloc(&c->d_k3_coffs, ((max_frames + kChunkMin - 1) / kChunkMin + 1) * (kChunkMaxNb + 1))) !=
+    // single-pass chunked scatter (batches of < kChunkMaxNb buckets): offsets of every
+    // chunk's buckets (4 B x 512 per 12288 frames)
+    if ((e = dalloc(&c->d_k3_coffs, ((max_frames + kChunk - 1) / kChunk + 1) * (kChunkMaxNb + 1))) !=
         hipSuccess)
       return fail(map_err(e));
   }
-  if (c->max_flows <= kFuseRankMax) {
+  if (c->max_flows <= kFuseRankMax && c->max_frames <= kRankSmallWords * 32) {
     // the second table generation and the second batch-state slot (K1 -> K3 scratch
-    // of both slots too: batches alternate slots from now on)
+    // of both slots too: batches alternate slots from now on). Only for contexts whose
+    // every batch can take the fused, prep-free path (<= kRankSmallWords * 32 = 1M
+    // frames): a small-flow context with a larger max_frames would double
+    // its 8 B/frame of scratch for batches that cannot use it
     c->small_gen = true;
     c->tab_alt = c->tab;
     c->tab_alt.slots = nullptr;
@@ -518,7 +521,7 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
   uint32_t* const acc_flow = c->d_slot_scratch_s[c->slot];
   uint32_t* const acc_len = c->d_len_scratch_s[c->slot];
   const int fpl = c->fpl;
-  const uint64_t tf = tile_frames(fpl, flows && fpl == 2 ? c->k1_variant : 0);
+  const uint64_t tf = tile_frames(fpl);
   const uint64_t ntiles = (in->n + tf - 1) / tf;
   const uint64_t nwords = flows && ntiles ? (in->n + 31) / 32 : 0;
   // a small context's batch that K2 would rank in one block: K3's blocks rank it
@@ -586,7 +589,7 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     a.out_frame = out_frame;
     const bool timed = c->profiling && c->ev_used < kMaxProfiled;
     if (timed) TRY_HIP(hipEventRecord(c->ev[2 * c->ev_used], s));
-    TRY_HIP(launch_parse(a, fpl, flows, s, c->k1_variant));
+    TRY_HIP(launch_parse(a, fpl, flows, s));
     if (timed) {
       TRY_HIP(hipEventRecord(c->ev[2 * c->ev_used + 1], s));
       ++c->ev_used;
@@ -611,7 +614,7 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     if (!fuse) TRY_HIP(launch_rank(r, s));
     CountArgs k{};
     k.fused_rank = fuse ? 1u : 0u;
-    k.wide_iter = in->n >= kK3WideFrames ? 1u : 0u;
+    k.wide_iter = (in->n >= kK3WideFrames || c->k3_wide) ? 1u : 0u;
     k.new_list = c->d_new_list;
     k.batch_rw = c->d_batch;
     k.tab = c->tab;
@@ -633,18 +636,12 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     k.part = c->d_count_part;
     k.range_ok = c->k3_range ? 1u : 0u;
     k.part_words = c->part_words;
-    k.scatter_unstaged = c->k3_variant == 90 ? 1u : 0u;  // TCBEE_K3ABL=90: A/B
     k.region = c->d_k3_region;
     k.offs = c->d_k3_offs;
     k.nb_max = c->k3_nb_max;
     k.lpart = c->d_k3_lpart;
     k.coffs = c->d_k3_coffs;
-    k.chunk_off = c->k3_variant == 91 ? 1u : 0u;  // TCBEE_K3ABL=91: the two-pass scatter (A/B)
-    // 12288-record chunks in 76 KiB of LDS (k_count_chunk2: two workgroups per CU).
-    // A/B: TCBEE_K3ABL=93 the round-2 k_count_chunk (16384 records, 132 KiB, one
-    // workgroup per CU); 92: its 8192-record form (512 threads, two per CU) — slower
-    // in round 2 than 16384: 125k flows 5.60 vs 5.72 ms/step, 1M flows 7.51 vs 7.77
-    k.chunk = (c->k3_variant == 92 || c->k3_variant == 95) ? 8192u : c->k3_variant == 93 ? 16384u : 12288u;
+    k.chunk_off = c->k3_twopass ? 1u : 0u;
     if (gen) {  // this K3 prepares the next batch (see skip_prep above)
       k.clean_tiles = c->d_tile_status;
       k.clean_ntiles = c->tiles_hw;
@@ -675,13 +672,6 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     uint64_t g1s = (in->n + 8191) / 8192;
     if (g1s > 2ull * c->n_cu) g1s = 2ull * c->n_cu;
     if (g1s == 0) g1s = 1;
-    if (async && c->async_k3_blocks) {
-      // A/B (TCBEE_ASYNC_K3_BLOCKS): a K3 beside the next K1 on fewer CUs
-      const uint64_t cap = c->async_k3_blocks;
-      if (g1 > cap && cap >= gmin) g1 = cap < 8 ? cap : cap / 8 * 8;
-      if (g1s > cap) g1s = cap;
-      k.g1 = (uint32_t)g1;
-    }
     if (defer) {
       c->pend = k;
       c->pend_g1 = (unsigned)g1;
@@ -697,8 +687,7 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
       TRY_HIP(hipStreamWaitEvent(ids_stream, c->ev_k2, 0));
       ks = ids_stream;
     }
-    TRY_HIP(launch_count(k, (unsigned)g1, (unsigned)g1s, c->d_k3_region ? c->k3_g2 : 0u, ks,
-                         c->k3_variant));
+    TRY_HIP(launch_count(k, (unsigned)g1, (unsigned)g1s, c->d_k3_region ? c->k3_g2 : 0u, ks));
     if (async) TRY_HIP(hipEventRecord(c->ev_k3, ks));
     c->k3_async = async;
     if (gen) {
@@ -738,7 +727,7 @@ int tcbee_parse_finish_device(tcbee_ctx* c, const uint32_t* id_map_dev, uint64_t
     k.omap = c->d_omap;
   }
   c->count_pending = false;
-  TRY_HIP(launch_count(k, c->pend_g1, c->pend_g1s, c->pend_g2, ks, c->k3_variant));
+  TRY_HIP(launch_count(k, c->pend_g1, c->pend_g1s, c->pend_g2, ks));
   if (c->pend_ids) TRY_HIP(hipEventRecord(c->ev_k3, ks));
   c->k3_async = c->pend_ids != nullptr;
   c->pend_ids = nullptr;

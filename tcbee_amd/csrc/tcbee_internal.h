@@ -151,7 +151,7 @@ struct RankArgs {
 
 // Launchers (tcbee_kernels.hip). All asynchronous on `s`.
 hipError_t launch_table_init(FlowTable t, hipStream_t s);
-hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s, int k1v = 0);
+hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s);
 hipError_t launch_rank(const RankArgs& r, hipStream_t s);
 struct CountArgs {
   uint64_t* out_n;           // finalize (block 0): record count, counters, running bases
@@ -175,7 +175,6 @@ struct CountArgs {
   uint32_t g1;               // k_count's grid (mode 3 eligibility: count_mode)
   uint32_t range_ok;         // mode 3 allowed (0: test hook / small table)
   uint64_t part_words;       // capacity of part (u64)
-  uint32_t scatter_unstaged; // mode 1 always by the lane-scattered pass 2 (A/B hook)
   // mode 1 (large tables; region == nullptr disables it)
   uint32_t* region;          // per accepted frame: claim within its bucket | caplen
                              // << kBucketBits (0 when >= kRegLenEsc: added by a global
@@ -183,13 +182,12 @@ struct CountArgs {
   uint32_t* offs;            // [g1s][nb_max + 1] bucket offsets inside each block's region
   uint32_t nb_max;           // buckets the context's table can need
   uint64_t* lpart;           // [S][nb * kBucket][2] partial pkts/bytes per claim
-  // mode 1, chunked (k_count_chunk; nb <= kSmallNb): the region is written chunk by
-  // chunk of kChunk records, bucket-sorted inside each chunk; coffs[q][0..nb] =
-  // bucket offsets inside chunk q (row stride kSmallNb + 1). nullptr: not used
+  // mode 1, chunked (k_count_chunk2; nb < kChunkMaxNb): the region is written chunk
+  // by chunk of kChunk records, bucket-sorted inside each chunk; coffs[q][0..nb] =
+  // bucket offsets inside chunk q (row stride kChunkMaxNb + 1). nullptr: not used
   uint32_t* coffs;
-  uint32_t chunk_off;        // 1: the two-pass scatter instead (A/B hook, TCBEE_K3ABL=91)
-  uint32_t chunk;            // records per chunk: 16384 (1024 threads, one workgroup per
-                             // CU) or 8192 (512 threads, two per CU; TCBEE_K3ABL=92, A/B)
+  uint32_t chunk_off;        // 1: the two-pass scatter instead (test hook,
+                             // TCBEE_TEST_K3_TWOPASS)
   // Fused rank (contexts of <= kFuseRankMax flows, batches K2 would rank in one
   // block): no rank launch — every k_count block ranks the batch's new flows itself
   // (mode 0 is certain), block 0 publishes cmap / cfs / flow_total and zeroes the new
@@ -217,8 +215,7 @@ constexpr uint64_t kFuseRankMax = 256;
 constexpr uint64_t kK3WideFrames = 16ull << 20;
 // g1 = k_count blocks; g1s = k_count_scatter blocks; g2 = k_count_bucket blocks
 // (g2 = 0: mode 1 impossible, neither is launched)
-hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned g2, hipStream_t s,
-                        int k3v = 0);
+hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned g2, hipStream_t s);
 
 struct MergeArgs {
   const uint64_t* ent;        // nseg * stride entries, tcbee_flow_entry as u64[8]
@@ -358,9 +355,11 @@ constexpr uint32_t kMaxBuckets = 4096;    // mode 1 up to 16M flows (hist + curs
 // 125k (31) +0.09 and 60k (15) +0.16 ms, where a wave's lanes already hit few
 // bucket cursors and the per-chunk barriers cost more than they save
 constexpr uint32_t kSmallNb = 512, kStagedMinNb = 64;
-// k_count_chunk's chunk: the records one workgroup sorts by bucket in LDS at a time
-// (16 per thread); the bucket pass sees chunk q as the segment [q * chunk, (q+1) * chunk)
-constexpr uint32_t kChunkMin = 8192;
+// k_count_chunk2's chunk: the records one 512-thread workgroup sorts by bucket in
+// LDS at a time (24 per thread, 76 KiB: two workgroups per CU); the bucket pass sees
+// chunk q as the segment [q * kChunk, (q+1) * kChunk)
+constexpr uint32_t kChunk = 12288;
+constexpr int kChunkBlock = 512;
 // chunked mode up to kChunkMaxNb - 1 buckets: the scan of nb + 1 counts takes one
 // per thread of the smaller (512-thread) workgroup
 constexpr uint32_t kChunkMaxNb = 511;

@@ -1,83 +1,35 @@
-// tcbee_kernels.hip — HIP kernels (gfx950) of the packet-record path.
+// tcbee_kernels.hip — HIP kernels (gfx950) of the packet-record path, K1-K3.
 //
 //   K1 k_parse     one lane per frame: bounds/ethertype/proto/port checks,
 //                  fixed-offset header extraction, the 74-B record, the flow
-//                  key + hash + flow-table upsert, and ORDER-PRESERVING
-//                  compaction of the records (decoupled look-back over dynamic
-//                  tiles), records staged in LDS and stored as 16-B vectors.
-//                  Restates xdp_hook / tc_hook (tcbee-ebpf/src/probes/xdp.rs:
-//                  27-223, tc.rs:28-183) + FLOWS insert (flow_tracker.rs:17-23)
-//                  + the drain task's serializer (tcbee/src/handlers/mod.rs:
+//                  key + hash + flow-table upsert (tcbee_table.h), and
+//                  ORDER-PRESERVING compaction of the records (decoupled look-back
+//                  over the tiles), records staged in LDS and stored as 16-B
+//                  vectors. Restates xdp_hook / tc_hook (tcbee-ebpf/src/probes/
+//                  xdp.rs:27-223, tc.rs:28-183) + FLOWS insert (flow_tracker.rs:
+//                  17-23) + the drain task's serializer (tcbee/src/handlers/mod.rs:
 //                  104-139).
-//   K2 k_mark / k_scan_words / k_scan_blocks / k_assign
+//   K2 k_rank_small | k_mark / k_scan_words / k_scan_blocks / k_assign
 //                  dense flow ids in first-seen order (the order in which
-//                  tcbee-process creates flows, db_writer.rs:51-65): a bitmap
-//                  over this batch's accepted frames marks each new flow's first
-//                  frame; id = popcount prefix.
-//   K3 k_gather    per record: slot -> dense id.
-//   k_finalize     counters (counters.rs) + record count + running bases.
-#include <hip/hip_runtime.h>
-
+//                  tcbee-process creates flows, db_writer.rs:51-65).
+//   K3 k_count (+ k_count_chunk2 / k_count_bucket, or the two-pass scatter, for
+//                  large tables) + k_count_reduce: per record claim -> output id,
+//                  pkts/bytes per flow; block 0 finalizes the counters
+//                  (counters.rs:43-83).
+// The N>1 exchange kernels are in tcbee_exchange.hip, the synthetic-trace
+// generators in tcbee_synth.hip.
 #include <cstdlib>
 
-#include "tcbee_gen.h"
-#include "tcbee_internal.h"
-#include "tcbee_layout.h"
+#include "tcbee_table.h"
 
 namespace tcbee {
 
-// ---------------------------------------------------------------------------
-// small device helpers
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Read at the coherence point (an RMW is never served from a stale cache).
-__device__ __forceinline__ uint64_t ld_coherent(uint64_t* p) {
-  return __hip_atomic_fetch_or(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
-__device__ __forceinline__ uint32_t bswap16(uint32_t v) {
-  return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu);
-}
-// bytes [r, r+4) of the 8-byte little-endian pair (lo, hi)
-__device__ __forceinline__ uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32_t r) {
-  return __builtin_amdgcn_alignbyte(hi, lo, r);
-}
-__device__ __forceinline__ uint64_t lanemask_lt() {
-  const uint32_t lane = __lane_id();
-  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
-}
-
-constexpr uint32_t kSpinLimit = 1u << 24;
 constexpr uint32_t kRecountSpins = 4096;  // ~0.1 ms of polling before recounting
-// K1's wave priority while a tile's index and header loads are issued (then 0).
-// Build-time knob for A/B libraries only (tools/lib_ab.sh, HIPEXTRA=-D...).
-#ifndef TCBEE_K1_LOAD_PRIO
-#define TCBEE_K1_LOAD_PRIO 2
-#endif
-constexpr int kK1LoadPrio = TCBEE_K1_LOAD_PRIO;
-// K3 (mode 0 k_count, mode 1 k_count_chunk2): the same load-phase priority around
-// each iteration's / chunk's record-word loads (0: off)
-#ifndef TCBEE_K3_LOAD_PRIO
-#define TCBEE_K3_LOAD_PRIO 0
-#endif
-constexpr int kK3LoadPrio = TCBEE_K3_LOAD_PRIO;
-// K1: a probe that misses its plain-load snapshot (a new flow, a slot still BUSY
-// with another lane's insert, a stale line) takes flow_upsert's coherent path
-// AFTER the tile's records are stored instead of before (the spin on a BUSY slot
-// then overlaps the record work; a cold table's first tiles all wait on a few
-// inserts). Build-time A/B knob (tools/lib_ab.sh, HIPEXTRA=-D...).
-#ifndef TCBEE_K1_DEFER_UPSERT
-#define TCBEE_K1_DEFER_UPSERT 0
-#endif
-constexpr bool kDeferUpsert = TCBEE_K1_DEFER_UPSERT != 0;
-[[maybe_unused]] constexpr int kAuxSc1 = 16;  // buffer cache-policy bits: sc1 (agent coherence, bypass L1)
-constexpr int kAuxPlain = 0;  // plain: L1/L2 allocating
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// K1's wave priority while a tile's index and header loads are issued (then 0):
+// a starting wave issues its loads ahead of resident waves' parse / record work
+// (config 3 K1 -2.6 %, round 3; priority 3 and a K3 load-phase priority measured
+// no different, round 4)
+constexpr int kK1LoadPrio = 2;
 
 // 16 bytes at arena[a .. a+16), zero past arena_len (a is 16-B aligned).
 __device__ __forceinline__ uint4 load_chunk(const uint8_t* arena, uint64_t arena_len, uint64_t a) {
@@ -103,19 +55,6 @@ __device__ __forceinline__ uint32_t clamp_caplen(uint64_t off, uint32_t caplen, 
   return caplen > arena_len - off ? (uint32_t)(arena_len - off) : caplen;
 }
 
-// streaming (non-temporal) access helpers: NT=true keeps the once-touched frame
-// stream and record stream from evicting the flow table's lines out of L2
-template <bool NT, class T>
-__device__ __forceinline__ T ld_stream(const T* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(p);
-  else return *p;
-}
-template <bool NT, class T>
-__device__ __forceinline__ void st_stream(T* p, T v) {
-  if constexpr (NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
-
 __device__ __forceinline__ void put_chunk(uint32_t (&w)[24], int c, uint4 v) {
   w[4 * c + 0] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
 }
@@ -125,42 +64,12 @@ __device__ __forceinline__ void put_chunk(uint32_t (&w)[24], int c, uint4 v) {
 // arena (the common case) all FPL x 5 loads are issued unconditionally, back to
 // back; otherwise each lane loads only the chunks of [off, off+min(len,54)),
 // bounds-checked. Chunk 5 (IPv6 tail) is loaded later, for IPv6 frames only.
-// Header-chunk load with an explicit cache policy (A/B of how the L2 fetches a
-// frame's header line; HPOL 0 = the compiler's plain load). Inline asm is not
-// tracked by the compiler's waitcnt insertion: load_windows waits explicitly.
-template <int HPOL>
-__device__ __forceinline__ u32x4 ld_hdr(const u32x4* p) {
-  u32x4 v;
-  if constexpr (HPOL == 1) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  else if constexpr (HPOL == 2) asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
-  else if constexpr (HPOL == 3) asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(v) : "v"(p) : "memory");
-  else if constexpr (HPOL == 4) asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1 nt" : "=v"(v) : "v"(p) : "memory");
-  else if constexpr (HPOL == 5) asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
-  else if constexpr (HPOL == 6) asm volatile("global_load_dwordx4 %0, %1, off sc0" : "=v"(v) : "v"(p) : "memory");
-  else v = *p;
-  return v;
-}
-
-template <int FPL, bool NOLOAD, bool NT = false, int HPOL = 0>
+// (Explicit cache policies nt / sc0 / sc1 on these loads fill the same 128-B lines
+// and were up to 20 % slower, round 2.)
+template <int FPL>
 __device__ __forceinline__ void load_windows(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                              const uint64_t (&off)[FPL], const uint32_t (&len)[FPL],
                                              uint32_t (&w)[FPL][24]) {
-  if (NOLOAD) {
-#pragma unroll
-    for (int f = 0; f < FPL; ++f) {
-      // timing ablation: a synthetic IPv4/TCP header (8192 flows) instead of the frame
-      const uint32_t fl = (uint32_t)(off[f] >> 6) & 8191u;
-#pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        uint4 v = make_uint4(0x01010101u * c, 0x02020202u * c + fl, 0x03030303u * c, 0x04040404u * c);
-        if (c == 0) v.w = 0x00450008u;  // ethertype 0x0800, ver/ihl 0x45
-        if (c == 1) v.y = 0x06400000u;  // ttl 64, proto 6
-        put_chunk(w[f], c, v);
-      }
-    }
-    __builtin_amdgcn_s_setprio(0);
-    return;
-  }
   bool inb = true;
 #pragma unroll
   for (int f = 0; f < FPL; ++f) inb = inb && (off[f] & ~15ull) + 80 <= arena_len;
@@ -180,16 +89,9 @@ __device__ __forceinline__ void load_windows(const uint8_t* __restrict__ arena, 
 #pragma unroll
       for (int c = 0; c < 5; ++c) {
         u32x4 v = {0u, 0u, 0u, 0u};
-        if ((uint32_t)c >= c_lo && (uint32_t)c <= c_hi)
-          v = HPOL ? ld_hdr<HPOL>(src + c) : ld_stream<NT>(src + c);
+        if ((uint32_t)c >= c_lo && (uint32_t)c <= c_hi) v = src[c];
         q[f][c] = v;
       }
-    }
-    if constexpr (HPOL != 0) {
-#pragma unroll
-      for (int f = 0; f < FPL; ++f)
-#pragma unroll
-        for (int c = 0; c < 5; ++c) asm volatile("s_waitcnt vmcnt(0)" : "+v"(q[f][c]) :: "memory");
     }
     __builtin_amdgcn_s_setprio(0);  // the tile's loads are issued: back to normal priority
 #pragma unroll
@@ -212,15 +114,14 @@ __device__ __forceinline__ void load_windows(const uint8_t* __restrict__ arena, 
   }
 }
 
-template <bool NOLOAD = false>
 __device__ __forceinline__ bool parse_window(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                              uint64_t off, uint32_t caplen, uint64_t ts,
                                              uint32_t filter_port, uint32_t (&w)[24],
                                              uint32_t (&R)[19], uint64_t (&K)[5]) {
   if (caplen < kEthHdrLen) return false;  // xdp.rs:37-39
   const uint64_t abase = off & ~15ull;
-  const uint32_t s = NOLOAD ? 0u : (uint32_t)(off & 15u);
-  if (!NOLOAD) {
+  const uint32_t s = (uint32_t)(off & 15u);
+  {
     // ethertype straight from the raw window: bytes s+12, s+13 (dwords 3..7)
     const uint32_t e = s + 12, t3 = (e >> 2) - 3, m1 = 0u - (t3 & 1u), m2 = 0u - ((t3 >> 1) & 1u);
     const uint32_t x0 = (w[3] & ~m1) | (w[4] & m1), x1 = (w[4] & ~m1) | (w[5] & m1);
@@ -329,217 +230,6 @@ __device__ __forceinline__ bool parse_window(const uint8_t* __restrict__ arena, 
 }
 
 // ---------------------------------------------------------------------------
-// Flow table (tcbee_internal.h): compact slot lines + per-claim entries.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t ld_agent32(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent32(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-constexpr uint64_t kKindBusy = 1ull << 56;
-constexpr uint64_t kClaimBits = 0xFFFFFFull << 32;  // w1 bits 55:32
-__device__ __forceinline__ uint32_t slot_line(uint32_t s) { return __umulhi(s, 0xAAAAAAABu) >> 1; }  // s / 3
-__device__ __forceinline__ uint64_t* slot_ptr(const FlowTable& T, uint32_t s) {
-  const uint32_t l = slot_line(s);
-  return T.slots + 8ull * l + 2u * (s - l * kSlotsPerLine);
-}
-__device__ __forceinline__ uint32_t* slot_fs(const FlowTable& T, uint32_t s) {
-  const uint32_t l = slot_line(s);
-  return reinterpret_cast<uint32_t*>(T.slots + 8ull * l + 6) + (s - l * kSlotsPerLine);
-}
-// home slot: line from the hash's high word (range reduction), position from its low bits
-__device__ __forceinline__ uint32_t home_slot(uint64_t h, uint64_t nlines) {
-  const uint32_t line = (uint32_t)(((h >> 32) * nlines) >> 32);
-  return line * kSlotsPerLine + (uint32_t)(((h & 0xFFFFFFull) * kSlotsPerLine) >> 24);
-}
-// the compact slot words that name an IPv4-form key K: w0 and the kind | lo32 bits
-// of w1 (all but the claim)
-__device__ __forceinline__ void key_slot_words(const uint64_t (&K)[5], uint64_t h, uint64_t& w0,
-                                               uint64_t& kl) {
-  (void)h;
-  w0 = (K[1] >> 32) | (K[3] & 0xFFFFFFFF00000000ull);
-  kl = (2ull << 56) | (uint32_t)K[4];  // sport | dport << 16 (protocol is always 6)
-}
-
-// first_seen (fs32) while a flow's first record index is not known yet: the
-// claimer stores kFs32Flag | its frame index, so later readers of a hot new flow
-// can tell locally whether they precede the claimer (and only those contend on the
-// atomicMin) instead of all seeing "unset". Batch-local: batches stay < 2^31 frames.
-__device__ __forceinline__ bool fs_needs_min(uint32_t fs_seen, uint32_t frame_i, uint32_t p) {
-  if (fs_seen & kFs32Flag) return (fs_seen & ~kFs32Flag) >= frame_i;  // the claimer or earlier
-  return p < fs_seen;
-}
-
-// the fs32 word of slot id s (compact or wide)
-__device__ __forceinline__ uint32_t* slot_fs_any(const FlowTable& T, uint32_t s) {
-  if (s & kWideSlot) return reinterpret_cast<uint32_t*>(T.wide + 8ull * (s & ~kWideSlot) + 6);
-  return slot_fs(T, s);
-}
-__device__ __forceinline__ bool key_is_v4form(const uint64_t (&K)[5]) {
-  return (K[0] | K[2] | (K[1] & 0xFFFFFFFFull) | (K[3] & 0xFFFFFFFFull)) == 0;
-}
-
-// Flow-table upsert; identity = the full 40-B key. Returns the slot id (~0 on
-// failure; wide slots carry kWideSlot); `claim` = the flow's claim index
-// (flow_count before this batch + its position in this batch's new-flow list),
-// fixed before the slot is published. A claim at or past max_claims is refused:
-// the slot is published dead (this key, no claim) so the flow's later frames find
-// it instead of claiming again, and the status reports TCBEE_EFLOWFULL.
-//
-// Compact slots (IPv4-form keys): CAS w1 empty -> busy, the entry (key) and the
-// slot's fs32 mark and w0 by agent-scope stores, drain, then w1 (agent-scope
-// store). The slot's line holds w0, w1 and fs32 together, so a snapshot that shows
-// a published w1 shows its w0 and mark, and the slot alone decides a match.
-__device__ uint32_t flow_upsert_compact(const FlowTable& T, const uint64_t (&K)[5], uint64_t h,
-                                        BatchState* batch, uint64_t* new_list,
-                                        PersistState* persist, uint64_t fbase, uint32_t& fs_seen,
-                                        uint32_t& claim, uint32_t claim_mark) {
-  uint64_t w0k, kl;
-  key_slot_words(K, h, w0k, kl);
-  const uint32_t nslots = (uint32_t)T.nlines * kSlotsPerLine;
-  uint32_t s = home_slot(h, T.nlines);
-  for (uint32_t probe = 0; probe < nslots; ++probe) {
-    uint64_t* m = slot_ptr(T, s);
-    uint64_t cur = ld_agent(m + 1);
-    if (cur == 0) {
-      uint64_t expected = 0;
-      if (__hip_atomic_compare_exchange_strong(m + 1, &expected, kKindBusy, __ATOMIC_RELAXED,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        const uint64_t slot_no = atomicAdd((unsigned long long*)&batch->n_new, 1ull);
-        const uint64_t cl = fbase + slot_no;
-        if (cl >= T.max_claims) {
-          st_agent(m, w0k);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          st_agent(m + 1, kl + (2ull << 56));  // dead
-          atomicOr(&persist->status, kStFlowFull);
-          return 0xFFFFFFFFu;
-        }
-        new_list[slot_no] = s;
-        claim = (uint32_t)cl;
-        uint64_t* e = T.ent + 8 * cl;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) st_agent(e + j, K[j]);
-        st_agent32(slot_fs(T, s), claim_mark);
-        st_agent(m, w0k);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        st_agent(m + 1, kl | (cl << 32));
-        fs_seen = claim_mark;
-        return s;
-      }
-      cur = expected;
-    }
-    for (uint32_t spins = 0; cur == kKindBusy; ++spins) {
-      if (spins > kSpinLimit) {
-        atomicOr(&persist->status, kStSpin);
-        return 0xFFFFFFFFu;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      cur = ld_agent(m + 1);
-    }
-    const uint64_t ckl = cur & ~kClaimBits;
-    if ((ckl == kl || ckl == kl + (2ull << 56)) && ld_agent(m) == w0k) {
-      if (ckl != kl) return 0xFFFFFFFFu;  // dead slot of this key: the table was full
-      fs_seen = ld_agent32(slot_fs(T, s));
-      claim = (uint32_t)((cur & kClaimBits) >> 32);
-      return s;
-    }
-    s = s + 1 == nslots ? 0u : s + 1;
-  }
-  atomicOr(&persist->status, kStFlowFull);
-  return 0xFFFFFFFFu;
-}
-
-// Wide slots (other keys): the rounds-1/2 protocol — CAS the tag word empty ->
-// busy, key (and entry) and the fs32 mark by agent-scope stores, drain, then the
-// tag word. Readers poll the tag relaxed and compare the key by agent-scope loads;
-// a mismatch is re-checked at the coherence point before the probe moves on
-// (never a duplicate flow).
-__device__ uint32_t flow_upsert_wide(const FlowTable& T, const uint64_t (&K)[5], uint64_t h,
-                                     BatchState* batch, uint64_t* new_list, PersistState* persist,
-                                     uint64_t fbase, uint32_t& fs_seen, uint32_t& claim,
-                                     uint32_t claim_mark) {
-  const uint32_t tag = hash_tag32(h);
-  uint64_t s = h & T.wide_mask;
-  for (uint64_t probe = 0; probe <= T.wide_mask; ++probe) {
-    uint64_t* m = T.wide + s * 8;
-    uint64_t cur = ld_agent(m);
-    if (cur == kTagEmpty) {
-      uint64_t expected = kTagEmpty;
-      if (__hip_atomic_compare_exchange_strong(m, &expected, kTagBusy, __ATOMIC_RELAXED,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        if (!ld_agent32(T.wide_used)) st_agent32(T.wide_used, 1u);
-#pragma unroll
-        for (int j = 0; j < 5; ++j) st_agent(m + 1 + j, K[j]);
-        // a context with fewer wide slots than max_flows (tcbee_ctx_create_ex) bounds
-        // its wide keys exactly: refused BEFORE a claim number is taken (claims stay
-        // dense), the slot published dead
-        const bool wide_full =
-            T.max_wide < T.max_claims &&
-            atomicAdd((unsigned long long*)&persist->wide_claims, 1ull) >= T.max_wide;
-        const uint64_t slot_no =
-            wide_full ? 0ull : atomicAdd((unsigned long long*)&batch->n_new, 1ull);
-        const uint64_t cl = wide_full ? T.max_claims : fbase + slot_no;
-        if (cl >= T.max_claims) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          st_agent(m, (uint64_t)tag | (0xFFFFFFFFull << 32));  // dead
-          atomicOr(&persist->status, kStFlowFull);
-          return 0xFFFFFFFFu;
-        }
-        new_list[slot_no] = (uint32_t)s | kWideSlot;
-        claim = (uint32_t)cl;
-        uint64_t* e = T.ent + 8 * cl;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) st_agent(e + j, K[j]);
-        st_agent(m + 6, (uint64_t)claim_mark);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        st_agent(m, (uint64_t)tag | (cl << 32));
-        fs_seen = claim_mark;
-        return (uint32_t)s | kWideSlot;
-      }
-      cur = expected;
-    }
-    for (uint32_t spins = 0; cur == kTagBusy; ++spins) {
-      if (spins > kSpinLimit) {
-        atomicOr(&persist->status, kStSpin);
-        return 0xFFFFFFFFu;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      cur = ld_agent(m);
-    }
-    if ((uint32_t)cur == tag) {
-      bool eq = true;
-#pragma unroll
-      for (int j = 0; j < 5; ++j) eq = eq && (ld_agent(m + 1 + j) == K[j]);
-      if (!eq) {
-        eq = true;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) eq = eq && (ld_coherent(m + 1 + j) == K[j]);
-      }
-      if (eq) {
-        if ((cur >> 32) == 0xFFFFFFFFull) return 0xFFFFFFFFu;  // dead: the table was full
-        fs_seen = (uint32_t)ld_agent(m + 6);
-        claim = (uint32_t)(cur >> 32);
-        return (uint32_t)s | kWideSlot;
-      }
-    }
-    s = (s + 1) & T.wide_mask;
-  }
-  atomicOr(&persist->status, kStFlowFull);
-  return 0xFFFFFFFFu;
-}
-
-__device__ __forceinline__ uint32_t flow_upsert(const FlowTable& T, const uint64_t (&K)[5], uint64_t h,
-                                                BatchState* batch, uint64_t* new_list,
-                                                PersistState* persist, uint64_t fbase,
-                                                uint32_t& fs_seen, uint32_t& claim,
-                                                uint32_t claim_mark = 0xFFFFFFFFu) {
-  return key_is_v4form(K)
-             ? flow_upsert_compact(T, K, h, batch, new_list, persist, fbase, fs_seen, claim, claim_mark)
-             : flow_upsert_wide(T, K, h, batch, new_list, persist, fbase, fs_seen, claim, claim_mark);
-}
-
-// ---------------------------------------------------------------------------
 // Decoupled look-back (one wave). Status word: bits 63:62 = 1 aggregate,
 // 2 inclusive prefix; bits 61:0 = value. Words are single 8-B agent-scope
 // stores polled by agent-scope loads (the data IS the flag).
@@ -629,7 +319,7 @@ __device__ __forceinline__ bool parse_frame(const uint8_t* __restrict__ arena, u
   const uint64_t o[1] = {off};
   const uint32_t l[1] = {clamp_caplen(off, caplen, arena_len)};
   uint32_t w[1][24];
-  load_windows<1, false>(arena, arena_len, o, l, w);
+  load_windows<1>(arena, arena_len, o, l, w);
   return parse_window(arena, arena_len, off, l[0], ts, filter_port, w[0], R, K);
 }
 
@@ -655,7 +345,6 @@ __device__ uint32_t tile_accept_count(const ParseArgs& a, uint64_t tile) {
 // Copies staged records [G0, G1) (global byte range; sbuf byte 0 = global byte G0)
 // to out: 16-B stores for whole chunks, 2-B stores for the partial chunks at the
 // ends (bytes there belong to neighbouring groups). Threads t0, t0+step, ...
-template <bool NT = false>
 __device__ __forceinline__ void copy_out(uint8_t* __restrict__ out, uint64_t G0, uint64_t G1,
                                          const uint32_t* sbuf, uint32_t t0, uint32_t step) {
   const uint64_t A = G0 & ~15ull;
@@ -678,7 +367,7 @@ __device__ __forceinline__ void copy_out(uint8_t* __restrict__ out, uint64_t G0,
       }
       u32x4 ov;
       ov[0] = o.x; ov[1] = o.y; ov[2] = o.z; ov[3] = o.w;
-      st_stream<NT>(reinterpret_cast<u32x4*>(out + g), ov);
+      *reinterpret_cast<u32x4*>(out + g) = ov;
     } else {
       const uint64_t lo = g > G0 ? g : G0;
       const uint64_t hi = (g + 16) < G1 ? (g + 16) : G1;
@@ -688,32 +377,17 @@ __device__ __forceinline__ void copy_out(uint8_t* __restrict__ out, uint64_t G0,
   }
 }
 
-__device__ __forceinline__ void wave_lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
-
 // ---------------------------------------------------------------------------
 // K1
 // ---------------------------------------------------------------------------
-// ABL: timing-only ablation bits (0 in every product launch; see tools/ablate.py)
-//   1 no look-back, 2 no record stores, 4 no header loads, 8 no index loads,
-//   16 no side outputs, 32 no first-seen competition (atomicMin), 64 IPv4-form
-//   probes load a line of the table's first 16 MiB instead of their slot and take a
-//   hash-derived claim (what a probe served from a table small enough for the
-//   Infinity Cache would cost)
-// STAGE 0: the whole tile's records staged in LDS, stored by the block after the
-// look-back; STAGE 1: each wave stages and stores its own 64-record group per
-// round (its records are contiguous in the output), 4.7 KB of LDS per wave.
-// OCC: minimum waves per SIMD requested from the register allocator (0: default)
-template <int FPL, bool FLOWS, int PROBE_AUX, int ABL = 0, int STAGE = 0, bool NT = false, int OCC = 0,
-          int HPOL = 0, int BLK = kBlock>
-__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, OCC ? 8 : 8)))
-void k_parse(ParseArgs a) {
-  constexpr int TILE = BLK * FPL;
-  constexpr int NW = BLK / 64;  // waves per tile
-  constexpr int WBUF_DW = (64 * kRecBytes + 32) / 4;
-  constexpr int SREC_DW = STAGE ? NW * WBUF_DW : (TILE * kRecBytes + 32) / 4;
+// One tile of FPL x kBlock frames per block (tile = blockIdx.x). The tile's records
+// are staged in LDS at their compacted positions and stored by the whole block
+// after the look-back (a per-wave staging was slightly slower, round 2).
+template <int FPL, bool FLOWS>
+__global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
+  constexpr int TILE = kBlock * FPL;
+  constexpr int NW = kBlock / 64;  // waves per tile
+  constexpr int SREC_DW = (TILE * kRecBytes + 32) / 4;
   __shared__ __attribute__((aligned(16))) uint32_t s_rec[SREC_DW];
   __shared__ uint32_t s_wcnt[FPL][NW];
   __shared__ uint64_t s_excl;
@@ -739,7 +413,7 @@ void k_parse(ParseArgs a) {
   uint64_t offv[FPL], tsv[FPL];
 #pragma unroll
   for (int f = 0; f < FPL; ++f) {
-    const uint64_t i = i0 + (uint64_t)f * BLK + tid;
+    const uint64_t i = i0 + (uint64_t)f * kBlock + tid;
     acc[f] = false;
     slot[f] = 0xFFFFFFFFu;
     claim[f] = 0xFFFFFFFFu;
@@ -749,23 +423,22 @@ void k_parse(ParseArgs a) {
     for (int j = 0; j < 5; ++j) K[f][j] = 0;
     const bool in = i < a.n;
     const uint64_t ic = in ? i : a.n - 1;  // loads stay unconditional (no branch per frame)
-    const uint64_t o = (ABL & 8) ? ic * 64 : ld_stream<NT>(a.offset + ic);
-    const uint32_t l = (ABL & 8) ? 64u : ld_stream<NT>(a.caplen + ic);
-    const uint64_t t = (ABL & 8) ? ic : ld_stream<NT>(a.ts + ic);
+    const uint64_t o = a.offset[ic];
+    const uint32_t l = a.caplen[ic];
+    tsv[f] = a.ts[ic];
     offv[f] = in ? o : 0;
     clen[f] = in ? l : 0;
-    tsv[f] = t;
   }
   uint32_t lenc[FPL];
 #pragma unroll
   for (int f = 0; f < FPL; ++f) lenc[f] = clamp_caplen(offv[f], clen[f], a.arena_len);
   {
     uint32_t W[FPL][24];
-    load_windows<FPL, (ABL & 4) != 0, NT, HPOL>(a.arena, a.arena_len, offv, lenc, W);
+    load_windows<FPL>(a.arena, a.arena_len, offv, lenc, W);
 #pragma unroll
     for (int f = 0; f < FPL; ++f)
-      acc[f] = parse_window<(ABL & 4) != 0>(a.arena, a.arena_len, offv[f], lenc[f], tsv[f],
-                                            a.filter_port, W[f], R[f], K[f]);
+      acc[f] = parse_window(a.arena, a.arena_len, offv[f], lenc[f], tsv[f], a.filter_port, W[f],
+                            R[f], K[f]);
   }
 #pragma unroll
   for (int f = 0; f < FPL; ++f) {
@@ -789,33 +462,15 @@ void k_parse(ParseArgs a) {
   // (a.withhold_every: test hook, tiles t % k == k-1 never publish, forcing their
   //  successors down the recount path)
   const bool withhold = a.withhold_every && (tile % a.withhold_every) == a.withhold_every - 1;
-  if (!(ABL & 1) && !withhold && tid == 0) lookback_publish(a.tile_status, tile, total);
+  if (!withhold && tid == 0) lookback_publish(a.tile_status, tile, total);
 
-  // probe results per frame group (lane-private until publish_probe shares a
-  // wave-uniform key's leader result with its wave)
-  uint32_t psl[FPL], pcl[FPL], pfs[FPL];
-  bool pend[FPL], uni[FPL], want[FPL];
-  uint32_t leader[FPL];
-  uint64_t h[FPL];
-#pragma unroll
-  for (int f = 0; f < FPL; ++f) pend[f] = uni[f] = want[f] = false;
-  auto publish_probe = [&](int f) {
-    if (uni[f]) {
-      slot[f] = __shfl(psl[f], leader[f]);
-      claim[f] = __shfl(pcl[f], leader[f]);
-      fs_seen[f] = __shfl(pfs[f], leader[f]);
-    } else if (acc[f]) {
-      slot[f] = psl[f];
-      claim[f] = psl[f] == 0xFFFFFFFFu ? 0xFFFFFFFFu : pcl[f];
-      fs_seen[f] = pfs[f];
-    }
-  };
   if (FLOWS) {
     // phase B: hash, then issue the first probe's loads of every frame: an IPv4-form
     // key's 16-B compact slot + its fs32 (one line), any other key's 64-B wide slot
     u32x4 Q[FPL][4];
-    uint32_t FS[FPL], S0[FPL];
-    bool v4k[FPL];
+    uint32_t FS[FPL], S0[FPL], leader[FPL];
+    bool v4k[FPL], uni[FPL], want[FPL];
+    uint64_t h[FPL];
     // num_records = the slot lines' bytes (< 2^32: max_flows <= kMaxTableFlows; the
     // bits are read as unsigned), and the wide slots' (<= 2^31 bytes: see the ABI)
     const __amdgpu_buffer_rsrc_t sl_rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -842,22 +497,17 @@ void k_parse(ParseArgs a) {
         // miss falls through to flow_upsert's coherent path.
         if (v4k[f]) {
           S0[f] = home_slot(h[f], a.tab.nlines);
-          uint32_t l = slot_line(S0[f]), pos = S0[f] - l * kSlotsPerLine;
-          // probe window of the ceiling ablation: 64 = 16 MiB (Infinity-Cache resident),
-          // +128 = 2 MiB, +256 = 4 MiB, +384 = 512 KiB (L2-sized first levels)
-          constexpr uint32_t kAblWin = (ABL & 384) == 128 ? (2u << 20) : (ABL & 384) == 256 ? (4u << 20)
-                                     : (ABL & 384) == 384 ? (512u << 10) : (16u << 20);
-          if (ABL & 64) l = (uint32_t)(h[f] >> 40) & (kAblWin / 64u - 1u);
-          Q[f][0] = __builtin_amdgcn_raw_buffer_load_b128(sl_rs, l * 64u + 16u * pos, 0, PROBE_AUX);
+          const uint32_t l = slot_line(S0[f]), pos = S0[f] - l * kSlotsPerLine;
+          Q[f][0] = __builtin_amdgcn_raw_buffer_load_b128(sl_rs, l * 64u + 16u * pos, 0, 0);
           // (the slot and its fs32 share one 64-B half-line: the two halves of a
           //  128-B line can be of different ages in L1/L2 — a fresh published slot
           //  beside a stale fs32 lost first_seen values when fs32 sat in the other half)
-          FS[f] = __builtin_amdgcn_raw_buffer_load_b32(sl_rs, l * 64u + 48u + 4u * pos, 0, PROBE_AUX);
+          FS[f] = __builtin_amdgcn_raw_buffer_load_b32(sl_rs, l * 64u + 48u + 4u * pos, 0, 0);
         } else {
           S0[f] = (uint32_t)(h[f] & a.tab.wide_mask);
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            Q[f][j] = __builtin_amdgcn_raw_buffer_load_b128(wd_rs, S0[f] * 64u + 16u * j, 0, PROBE_AUX);
+            Q[f][j] = __builtin_amdgcn_raw_buffer_load_b128(wd_rs, S0[f] * 64u + 16u * j, 0, 0);
         }
       }
     }
@@ -867,6 +517,8 @@ void k_parse(ParseArgs a) {
     // published foreign slot seen in any snapshot is foreign for good; EMPTY/BUSY may
     // be stale and end the walk. A wide slot whose tag equals ours but whose key
     // differs goes to the coherent path (it may be a stale snapshot of our flow).
+    // (Resolving a snapshot miss after the tile's records are stored instead was no
+    //  faster, round 4.)
     const uint32_t nslots = (uint32_t)a.tab.nlines * kSlotsPerLine;
 #pragma unroll
     for (int f = 0; f < FPL; ++f) {
@@ -880,15 +532,7 @@ void k_parse(ParseArgs a) {
           uint64_t w0 = (uint64_t)Q[f][0][0] | ((uint64_t)Q[f][0][1] << 32);
           uint64_t w1 = (uint64_t)Q[f][0][2] | ((uint64_t)Q[f][0][3] << 32);
           uint32_t fsv = FS[f];
-          if (ABL & 64) {
-            asm volatile("" ::"v"(Q[f][0][0]), "v"(fsv));
-            sl = s;
-            cl = (uint32_t)(h[f] % a.tab.max_claims);
-            fs = 0xFFFFFFFFu;
-            slow = false;
-            w1 = 0;  // skip the walk
-          }
-          for (uint32_t step = 0; !(ABL & 64); ++step) {
+          for (uint32_t step = 0;; ++step) {
             if (w1 <= kKindBusy) break;
             if ((w1 & ~kClaimBits) == kl && w0 == w0k) {  // the whole key: a hit
               sl = s;
@@ -900,8 +544,8 @@ void k_parse(ParseArgs a) {
             if (step >= a.plain_walk) break;
             s = s + 1 == nslots ? 0u : s + 1;
             const uint32_t l = slot_line(s), pos = s - l * kSlotsPerLine;
-            const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(sl_rs, l * 64u + 16u * pos, 0, PROBE_AUX);
-            fsv = __builtin_amdgcn_raw_buffer_load_b32(sl_rs, l * 64u + 48u + 4u * pos, 0, PROBE_AUX);
+            const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(sl_rs, l * 64u + 16u * pos, 0, 0);
+            fsv = __builtin_amdgcn_raw_buffer_load_b32(sl_rs, l * 64u + 48u + 4u * pos, 0, 0);
             w0 = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
             w1 = (uint64_t)q[2] | ((uint64_t)q[3] << 32);
           }
@@ -930,7 +574,7 @@ void k_parse(ParseArgs a) {
             s = (uint32_t)((s + 1) & a.tab.wide_mask);
             u32x4 q[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) q[j] = __builtin_amdgcn_raw_buffer_load_b128(wd_rs, s * 64u + 16u * j, 0, PROBE_AUX);
+            for (int j = 0; j < 4; ++j) q[j] = __builtin_amdgcn_raw_buffer_load_b128(wd_rs, s * 64u + 16u * j, 0, 0);
 #pragma unroll
             for (int j = 0; j < 7; ++j) {
               const u32x4 v = q[j >> 1];
@@ -938,34 +582,30 @@ void k_parse(ParseArgs a) {
             }
           }
         }
-        if (slow && !kDeferUpsert)
+        if (slow)
           sl = flow_upsert(a.tab, K[f], h[f], a.batch, a.new_list, a.persist, fbase, fs, cl,
-                           kFs32Flag | (uint32_t)(i0 + (uint64_t)f * BLK + tid));
-        pend[f] = slow && kDeferUpsert;
+                           kFs32Flag | (uint32_t)(i0 + (uint64_t)f * kBlock + tid));
       }
-      psl[f] = sl;
-      pcl[f] = cl;
-      pfs[f] = fs;
-      if (!kDeferUpsert) publish_probe(f);
+      // a wave-uniform key: the leader's result for the whole wave
+      if (uni[f]) {
+        slot[f] = __shfl(sl, leader[f]);
+        claim[f] = __shfl(cl, leader[f]);
+        fs_seen[f] = __shfl(fs, leader[f]);
+      } else if (acc[f]) {
+        slot[f] = sl;
+        claim[f] = sl == 0xFFFFFFFFu ? 0xFFFFFFFFu : cl;
+        fs_seen[f] = fs;
+      }
     }
   }
-  if (!(ABL & 2)) {
-    if (STAGE == 0) {
 #pragma unroll
-      for (int f = 0; f < FPL; ++f)
-        if (acc[f]) lds_put_record(s_rec, rank[f] * kRecBytes, R[f]);
-    }
-  } else {
-#pragma unroll
-    for (int f = 0; f < FPL; ++f)
-      if (acc[f]) asm volatile("" ::"v"(R[f][0]), "v"(R[f][5]), "v"(R[f][13]), "v"(R[f][17]));
-  }
+  for (int f = 0; f < FPL; ++f)
+    if (acc[f]) lds_put_record(s_rec, rank[f] * kRecBytes, R[f]);
 
   // (wave 0 resolving the look-back before its own probes instead — its inclusive
   //  prefix published a probe phase earlier — was 22 % slower, round 3)
   if (wave == 0) {
-    const uint64_t excl =
-        (ABL & 1) ? tile * (uint64_t)TILE : lookback_resolve<TILE>(a, tile, total, withhold);
+    const uint64_t excl = lookback_resolve<TILE>(a, tile, total, withhold);
     if (lane == 0) s_excl = excl;
   }
   __syncthreads();
@@ -973,41 +613,11 @@ void k_parse(ParseArgs a) {
   if (tid == 0 && tile == a.ntiles - 1) a.batch->n_acc = excl + total;
 
   // ---- records: LDS -> HBM, 16-B stores, partial chunks as 2-B stores ----
-  if (!(ABL & 2)) {
-    if (STAGE == 0) {
-      const uint64_t wr_lo = excl < a.out_cap ? excl : a.out_cap;
-      const uint64_t wr_hi = (excl + total) < a.out_cap ? (excl + total) : a.out_cap;
-      if (wr_hi > wr_lo)
-        copy_out<NT>(a.out_rec, wr_lo * kRecBytes, wr_hi * kRecBytes, s_rec, tid, BLK);
-    } else {
-      uint32_t* wbuf = s_rec + wave * WBUF_DW;
-#pragma unroll
-      for (int f = 0; f < FPL; ++f) {
-        const uint64_t b = __ballot(acc[f]);
-        const uint32_t lrank = (uint32_t)__popcll(b & lanemask_lt());
-        const uint64_t g0 = excl + rank[f] - lrank;  // this wave's group start
-        const uint64_t g1 = g0 + (uint64_t)__popcll(b);
-        const uint64_t lo = g0 < a.out_cap ? g0 : a.out_cap;
-        const uint64_t hi = g1 < a.out_cap ? g1 : a.out_cap;
-        if (hi > lo) {
-          if (acc[f]) lds_put_record(wbuf, lrank * kRecBytes, R[f]);
-          wave_lds_sync();
-          copy_out<NT>(a.out_rec, lo * kRecBytes, hi * kRecBytes, wbuf, lane, 64);
-          wave_lds_sync();
-        }
-      }
-    }
-  }
-
-  if (FLOWS && kDeferUpsert) {
-    // the probes whose snapshot missed, after the records are out
-#pragma unroll
-    for (int f = 0; f < FPL; ++f) {
-      if (want[f] && pend[f])
-        psl[f] = flow_upsert(a.tab, K[f], h[f], a.batch, a.new_list, a.persist, fbase, pfs[f],
-                             pcl[f], kFs32Flag | (uint32_t)(i0 + (uint64_t)f * BLK + tid));
-      publish_probe(f);
-    }
+  // (non-temporal record stores were slower, round 1)
+  {
+    const uint64_t wr_lo = excl < a.out_cap ? excl : a.out_cap;
+    const uint64_t wr_hi = (excl + total) < a.out_cap ? (excl + total) : a.out_cap;
+    if (wr_hi > wr_lo) copy_out(a.out_rec, wr_lo * kRecBytes, wr_hi * kRecBytes, s_rec, tid, kBlock);
   }
 
   // ---- per-record side outputs; first_seen = min accepted index ----
@@ -1017,26 +627,25 @@ void k_parse(ParseArgs a) {
 #pragma unroll
   for (int f = 0; f < FPL; ++f) {
     const uint64_t p = excl + rank[f];
-    if (acc[f] && !(ABL & 16)) {
-      if (a.out_hash && p < a.out_cap) st_stream<NT>(a.out_hash + p, hsh[f]);
+    if (acc[f]) {
+      if (a.out_hash && p < a.out_cap) a.out_hash[p] = hsh[f];
       // record -> frame map (flow-hash shards of traces with rejected frames)
-      if (a.out_frame && p < a.out_cap) st_stream<NT>(a.out_frame + p, (uint32_t)(i0 + (uint64_t)f * BLK + tid));
+      if (a.out_frame && p < a.out_cap) a.out_frame[p] = (uint32_t)(i0 + (uint64_t)f * kBlock + tid);
       if (FLOWS) {
         if (a.pack_bits) {
           // (claim, caplen) in one word; a caplen that does not fit saturates the
           // field and is stored in full beside it (K3 reads it only then)
           const uint32_t lmax = 0xFFFFFFFFu >> a.pack_bits;
           const uint32_t lq = clen[f] < lmax ? clen[f] : lmax;
-          st_stream<NT>(a.acc_flow + p, claim[f] == 0xFFFFFFFFu ? 0xFFFFFFFFu
-                                                                : claim[f] | (lq << a.pack_bits));
+          a.acc_flow[p] = claim[f] == 0xFFFFFFFFu ? 0xFFFFFFFFu : claim[f] | (lq << a.pack_bits);
           if (lq == lmax) a.acc_len[p] = clen[f];
         } else {
-          st_stream<NT>(a.acc_flow + p, claim[f]);
-          st_stream<NT>(a.acc_len + p, clen[f]);
+          a.acc_flow[p] = claim[f];
+          a.acc_len[p] = clen[f];
         }
       }
     }
-    if (FLOWS && !(ABL & 32)) {
+    if (FLOWS) {
       // first_seen competition: only flows new in this batch (claim >= fbase)
       const bool mine = acc[f] && slot[f] != 0xFFFFFFFFu && claim[f] >= fbase;
       const uint64_t am = __ballot(mine);
@@ -1044,7 +653,7 @@ void k_parse(ParseArgs a) {
         const uint32_t leader = (uint32_t)__ffsll((unsigned long long)am) - 1;
         const uint32_t s0 = __shfl(slot[f], leader);
         const uint32_t p32 = (uint32_t)p;
-        const uint32_t frame_i = (uint32_t)(i0 + (uint64_t)f * BLK + tid);
+        const uint32_t frame_i = (uint32_t)(i0 + (uint64_t)f * kBlock + tid);
         if (__all(!mine || slot[f] == s0)) {
           // leader = lowest rank of the wave = its smallest accepted index; when the
           // wave's previous frame group was all this slot too, its earlier leader
@@ -1284,27 +893,6 @@ __device__ __forceinline__ uint64_t rank_words(const RankArgs& r) {
   return m < r.nwords ? m : r.nwords;
 }
 
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp, uint32_t& total) {
-  // 256 threads, 4 waves
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o);
-    if (lane >= (uint32_t)o) x += y;
-  }
-  if (lane == 63) s_tmp[wave] = x;
-  __syncthreads();
-  uint32_t wbase = 0;
-  total = 0;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    if ((uint32_t)w < wave) wbase += s_tmp[w];
-    total += s_tmp[w];
-  }
-  __syncthreads();
-  return wbase + x - v;
-}
 
 __global__ __launch_bounds__(kBlock) void k_scan_words(RankArgs r) {
   __shared__ uint32_t s_tmp[4];
@@ -1463,43 +1051,6 @@ __device__ __forceinline__ void load_acc(const CountArgs& c, uint64_t p0, uint64
   }
 }
 
-// The same for packed words, four consecutive records per 16-B load: entry 4k + j
-// is record p0 + 4 k kCountBlock + j (p0 = base + 4 tid, 16-B aligned: block ranges
-// start at multiples of kK3Gran). Four times the bytes in flight per load
-// instruction of the scalar form (K3 mode 0 holds one 1024-thread block per CU).
-template <int U>
-__device__ __forceinline__ void load_acc4(const CountArgs& c, uint64_t p0, uint64_t hi,
-                                          uint32_t (&claim)[4 * U], uint32_t (&len)[4 * U]) {
-  uint32_t v[4 * U];
-#pragma unroll
-  for (int k = 0; k < U; ++k) {
-    const uint64_t p = p0 + 4ull * k * kCountBlock;
-    if (p + 3 < hi) {
-      const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(c.acc_flow + p));
-      v[4 * k] = q[0];
-      v[4 * k + 1] = q[1];
-      v[4 * k + 2] = q[2];
-      v[4 * k + 3] = q[3];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[4 * k + j] = p + j < hi ? c.acc_flow[p + j] : 0xFFFFFFFFu;
-    }
-  }
-  const uint32_t lmax = 0xFFFFFFFFu >> c.pack_bits;
-  bool sat = false;
-#pragma unroll
-  for (int e = 0; e < 4 * U; ++e) {
-    claim[e] = v[e] == 0xFFFFFFFFu ? v[e] : (v[e] & ((1u << c.pack_bits) - 1u));
-    len[e] = v[e] == 0xFFFFFFFFu ? 0u : v[e] >> c.pack_bits;
-    sat |= len[e] == lmax;
-  }
-  if (__any(sat)) {  // a caplen past the packed field: the side array (rare)
-#pragma unroll
-    for (int e = 0; e < 4 * U; ++e)
-      if (len[e] == lmax) len[e] = c.acc_len[p0 + 4ull * (e / 4) * kCountBlock + (e % 4)];
-  }
-}
-
 template <bool PACK>
 __device__ __forceinline__ uint32_t load_claim(const CountArgs& c, uint64_t p) {
   const uint32_t v = __builtin_nontemporal_load(&c.acc_flow[p]);
@@ -1536,9 +1087,7 @@ __device__ __forceinline__ uint32_t block1024_excl_scan(uint32_t v, uint32_t* s_
   return base + x - v;
 }
 
-// Mode 1, phase 1 (inside k_count): ids out, bucket counts, scan, scatter.
-// SABL (timing-only ablations, 0 in product launches): 1 no region stores,
-// 2 no second pass, 4 no id gather/stores in the first pass
+// Mode 1, phase 1 (tables past the chunked pass): ids out, bucket counts, scan, scatter.
 // STAGED (nb <= kSmallNb): pass 2 counting-sorts each chunk of U x 1024 entries
 // by bucket in LDS (stage / sb / ch / co) and stores them as per-bucket runs.
 struct ScatterStage {
@@ -1548,7 +1097,7 @@ struct ScatterStage {
   uint32_t* co;     // [kSmallNb + 1] chunk offsets per bucket
 };
 
-template <int U, bool PACK, int SABL = 0, bool STAGED = false>
+template <int U, bool PACK, bool STAGED = false>
 __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint64_t nflows,
                               uint32_t* hist, uint32_t* cur, uint32_t* s_w,
                               const ScatterStage& st = ScatterStage{}) {
@@ -1571,7 +1120,7 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
       s[k] = load_claim<PACK>(c, p < hi ? p : lo);
       if (p >= hi) s[k] = 0xFFFFFFFFu;
     }
-    if (!(SABL & 4)) {
+    {
       uint32_t id[U];
 #pragma unroll
       for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.omap[s[k]];
@@ -1584,10 +1133,6 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
     // no-flow records bump the spare counter hist[kMaxBuckets]: no branch per record
 #pragma unroll
     for (int k = 0; k < U; ++k) {
-      if (SABL & 8) {
-        asm volatile("" ::"v"(s[k]));
-        continue;
-      }
       atomicAdd(&hist[s[k] != 0xFFFFFFFFu ? (s[k] >> kBucketBits) : kMaxBuckets], 1u);
     }
   }
@@ -1606,7 +1151,6 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
   }
   if (tid == 0) offs[nb] = total;
   __syncthreads();
-  if (SABL & 2) return;
   if constexpr (STAGED) {
     for (uint32_t b = tid; b <= kMaxBuckets; b += kCountBlock) st.ch[b] = 0;
     __syncthreads();
@@ -1660,13 +1204,6 @@ __device__ void count_scatter(const CountArgs& c, uint64_t lo, uint64_t hi, uint
 #pragma unroll
     for (int k = 0; k < U; ++k)
       pos[k] = atomicAdd(&cur[s[k] != 0xFFFFFFFFu ? (s[k] >> kBucketBits) : kMaxBuckets], 1u);
-    if (SABL & 1) {
-      uint32_t x = 0;
-#pragma unroll
-      for (int k = 0; k < U; ++k) x ^= pos[k] ^ len[k];
-      asm volatile("" ::"v"(x));
-      continue;
-    }
 #pragma unroll
     for (int k = 0; k < U; ++k)
       if (s[k] != 0xFFFFFFFFu)
@@ -1786,13 +1323,14 @@ __device__ uint64_t fused_rank_block(const CountArgs& c, uint32_t* s_map, uint64
   return fbase + n_new;
 }
 
-// ABL3 (timing-only ablations, 0 in every product launch): 1 no bin updates,
-// 2 no id gather, 4 no id stores; 8 (A/B, variants build) plain id stores instead of
-// non-temporal ones.
 // Bins are indexed by CLAIM (dense in [0, F)); the record's output id is
 // omap[claim] (the local dense id, or — after a flow-hash exchange — the global
 // one), staged in LDS; k_count_reduce maps claims to local ids for the counters.
-template <int U, int ABL3, bool PACK, bool VEC = false>
+// U records per lane and iteration: 8, or 16 on batches of >= kK3WideFrames (twice
+// the loads in flight). (16-B loads of four packed words, buffer-addressed 16/24-record
+// iterations and plain id stores were measured no faster, round 4: K3 mode 0 is bound
+// by its id stores, which serialize with the record-word reads.)
+template <int U, bool PACK>
 __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
   __shared__ uint64_t s_bin[kCountBins];  // by claim
   __shared__ uint32_t s_map[kCountBins];  // claim index -> output id
@@ -1849,60 +1387,22 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
     atomicAdd((unsigned long long*)&c.cnt[2ull * lid], (unsigned long long)pk);
     atomicAdd((unsigned long long*)&c.cnt[2ull * lid + 1], (unsigned long long)by);
   };
-  // VEC: four consecutive records per lane and load (packed words only)
-  constexpr int UU = VEC ? 4 * U : U;
-  for (uint64_t base = lo; base < hi; base += (uint64_t)UU * kCountBlock) {
-    uint32_t s[UU], len[UU], id[UU];
-    if (kK3LoadPrio) __builtin_amdgcn_s_setprio(kK3LoadPrio);
-    if constexpr (VEC) load_acc4<U>(c, base + 4ull * tid, hi, s, len);  // non-temporal
-    else load_acc<U, PACK>(c, base + tid, lo, hi, s, len);  // streamed once: non-temporal
-    if (kK3LoadPrio) __builtin_amdgcn_s_setprio(0);
-    if (ABL3 & 2) {
+  for (uint64_t base = lo; base < hi; base += (uint64_t)U * kCountBlock) {
+    uint32_t s[U], len[U], id[U];
+    load_acc<U, PACK>(c, base + tid, lo, hi, s, len);  // streamed once: non-temporal
+    if (mode == 0) {
 #pragma unroll
-      for (int k = 0; k < UU; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : (s[k] & 8191u);
-    } else if (mode == 0) {
-#pragma unroll
-      for (int k = 0; k < UU; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : s_map[s[k]];
+      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : s_map[s[k]];
     } else {
 #pragma unroll
-      for (int k = 0; k < UU; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.omap[s[k]];
+      for (int k = 0; k < U; ++k) id[k] = s[k] == 0xFFFFFFFFu ? 0xFFFFFFFFu : c.omap[s[k]];
     }
-    if (c.out_id && !(ABL3 & 4)) {
-      if constexpr (VEC) {
-        const uint64_t lim = hi < c.out_cap ? hi : c.out_cap;
+    if (c.out_id) {
 #pragma unroll
-        for (int k = 0; k < U; ++k) {
-          const uint64_t p = base + 4ull * ((uint64_t)k * kCountBlock + tid);
-          if (p + 3 < lim) {
-            u32x4 q;
-            q[0] = id[4 * k];
-            q[1] = id[4 * k + 1];
-            q[2] = id[4 * k + 2];
-            q[3] = id[4 * k + 3];
-            __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(c.out_id + p));
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (p + j < lim) c.out_id[p + j] = id[4 * k + j];
-          }
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-          const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
-          if (p < hi && p < c.out_cap) {
-            if constexpr ((ABL3 & 8) != 0) c.out_id[p] = id[k];
-            else __builtin_nontemporal_store(id[k], &c.out_id[p]);
-          }
-        }
+      for (int k = 0; k < U; ++k) {
+        const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
+        if (p < hi && p < c.out_cap) __builtin_nontemporal_store(id[k], &c.out_id[p]);
       }
-    }
-    if (ABL3 & 1) {
-      uint32_t x = 0;
-#pragma unroll
-      for (int k = 0; k < UU; ++k) x ^= id[k] ^ len[k];
-      asm volatile("" ::"v"(x));
-      continue;
     }
     if (mode == 0) {
       // one flow in all of the wave's records this iteration (a hot flow): one add
@@ -1910,20 +1410,20 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
       bool same = s0 != 0xFFFFFFFFu;
       uint32_t nk = 0, sl = 0;
 #pragma unroll
-      for (int k = 0; k < UU; ++k) {
+      for (int k = 0; k < U; ++k) {
         const bool v = s[k] != 0xFFFFFFFFu;
         same = same && (!v || (s[k] == s0 && len[k] < kBigLen));
         nk += v ? 1u : 0u;
         sl += v ? len[k] : 0u;
       }
       if (__all(same)) {
-        // pk <= 64*UU, by <= 64*UU*(kBigLen-1) < 2^32 at UU <= 32 (sums in 64 bits)
+        // pk <= 64*U, by <= 64*U*(kBigLen-1) < 2^32 at U <= 32 (sums in 64 bits)
         const uint64_t pk = wave_sum64(nk), by = wave_sum64(sl);
         if (lane == 0)
           atomicAdd((unsigned long long*)&s_bin[s0], ((unsigned long long)pk << kBinPkShift) | by);
       } else {
 #pragma unroll
-        for (int k = 0; k < UU; ++k) {
+        for (int k = 0; k < U; ++k) {
           if (s[k] == 0xFFFFFFFFu) continue;
           if (len[k] < kBigLen)
             atomicAdd((unsigned long long*)&s_bin[s[k]], (1ull << kBinPkShift) | len[k]);
@@ -1933,7 +1433,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < UU; ++k) {
+      for (int k = 0; k < U; ++k) {
         const bool mine = s[k] != 0xFFFFFFFFu;
         const uint64_t am = __ballot(mine);
         const uint32_t leader = am ? (uint32_t)__ffsll((unsigned long long)am) - 1 : 0u;
@@ -1975,6 +1475,12 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
         atomicAdd((unsigned long long*)&c.cnt[2ull * id + 1], (unsigned long long)(v & kBinByMask));
       }
     }
+    // Invariant: no block reads persist after its k3_done add. Every
+    // read of rec_base / flow_count in this kernel happens before the __syncthreads
+    // above, whose workgroup release waits for the block's outstanding loads, so a
+    // relaxed add suffices: the last block's writes below cannot reach a read that
+    // some block has not completed (no agent-scope release, which would write back
+    // the XCD's L2, is needed for that ordering).
     if (tid == 0 &&
         atomicAdd((unsigned long long*)&c.batch_rw->k3_done, 1ull) == (unsigned long long)gridDim.x - 1) {
       c.persist_rw->rec_base += n_acc;
@@ -1991,7 +1497,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count(CountArgs c) {
 
 // Mode 1, phase 1 as its own launch: 32 KiB of LDS, so two workgroups share a CU
 // (k_count's 144 KiB of bins + map allow one).
-// the single-pass chunked scatter (k_count_chunk) takes every mode-1 batch of up to
+// the single-pass chunked scatter (k_count_chunk2) takes every mode-1 batch of up to
 // kChunkMaxNb - 1 buckets when the context has its chunk offsets
 __device__ __forceinline__ bool chunk_scatter(const CountArgs& c, uint64_t nflows) {
   const uint64_t nb = (nflows + kBucket - 1) >> kBucketBits;
@@ -1999,10 +1505,10 @@ __device__ __forceinline__ bool chunk_scatter(const CountArgs& c, uint64_t nflow
 }
 __device__ __forceinline__ bool staged_scatter(const CountArgs& c, uint64_t nflows) {
   const uint64_t nb = (nflows + kBucket - 1) >> kBucketBits;
-  return !c.scatter_unstaged && nb >= kStagedMinNb && nb <= kSmallNb && !chunk_scatter(c, nflows);
+  return nb >= kStagedMinNb && nb <= kSmallNb && !chunk_scatter(c, nflows);
 }
 
-template <int U, bool PACK, int SABL = 0>
+template <int U, bool PACK>
 __global__ __launch_bounds__(kCountBlock) void k_count_scatter(CountArgs c) {
   __shared__ uint32_t s_hist[kMaxBuckets + 1], s_cur[kMaxBuckets + 1];  // + spare counter
   __shared__ uint32_t s_w[kCountBlock / 64];
@@ -2013,7 +1519,7 @@ __global__ __launch_bounds__(kCountBlock) void k_count_scatter(CountArgs c) {
   const uint64_t per = count_per(n_acc, gridDim.x);
   const uint64_t lo = (uint64_t)blockIdx.x * per < n_acc ? (uint64_t)blockIdx.x * per : n_acc;
   const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
-  count_scatter<U, PACK, SABL>(c, lo, hi, nflows, s_hist, s_cur, s_w);
+  count_scatter<U, PACK>(c, lo, hi, nflows, s_hist, s_cur, s_w);
 }
 
 // The same for tables of kStagedMinNb..kSmallNb buckets, pass 2 staged through LDS: 4 KiB of
@@ -2033,179 +1539,40 @@ __global__ __launch_bounds__(kCountBlock) void k_count_scatter_staged(CountArgs 
   const uint64_t lo = (uint64_t)blockIdx.x * per < n_acc ? (uint64_t)blockIdx.x * per : n_acc;
   const uint64_t hi = lo + per < n_acc ? lo + per : n_acc;
   ScatterStage st{s_stage, s_sb, s_ch, s_co};
-  count_scatter<U, PACK, 0, true>(c, lo, hi, nflows, s_hist, s_cur, s_w, st);
+  count_scatter<U, PACK, true>(c, lo, hi, nflows, s_hist, s_cur, s_w, st);
 }
 
-// Mode 1, single pass (nb < kChunkMaxNb): each workgroup takes chunks of c.chunk
-// accepted records (16 per thread) and
+// Mode 1, single pass (nb < kChunkMaxNb): each 512-thread workgroup takes chunks of
+// kChunk = 12288 accepted records (24 per thread) and
 //  1. ranks them by bucket in LDS (counts per bucket, one LDS add per record or one
 //     per wave when the wave's records share a bucket; no-flow records go to a
 //     spare bucket nb), scans the counts;
-//  2. places every record's region entry (claim within the bucket | caplen) and its
-//     chunk position + bucket at its bucket-sorted slot in LDS;
+//  2. places every record's chunk position at its bucket-sorted slot in LDS;
 //  3. walks the sorted entries with consecutive lanes on consecutive entries: the
-//     region entry is stored coalesced at region[chunk + idx] (the chunk's buckets
-//     are contiguous runs; coffs[q] = their offsets for k_count_bucket) and the
-//     claim -> output id gather reads omap inside one bucket's 16 KiB window per
-//     wave (L1-local), where the record-order gather of the two-pass scatter hit 64
-//     random lines of a table of every flow;
+//     region entry (claim within the bucket | caplen) is stored coalesced at
+//     region[chunk + idx] (the chunk's buckets are contiguous runs; coffs[q] = their
+//     offsets for k_count_bucket) and the claim -> output id gather reads omap inside
+//     one bucket's 16 KiB window per wave, where a record-order gather hits random
+//     lines of a table of every flow;
 //  4. writes each id back to its record position in LDS and stores the chunk's ids
 //     in record order, coalesced.
 // One pass over the K1 -> K3 words, no per-block cursors, no scattered stores.
-template <bool PACK, int BS>
-__global__ __launch_bounds__(BS) void k_count_chunk(CountArgs c) {
-  constexpr int U = 16, CH = U * BS;  // records per chunk (c.chunk)
-  __shared__ uint32_t s_ent[CH];   // region entries, bucket-sorted; then ids by position
-  __shared__ uint32_t s_pb[CH];    // chunk position | bucket << 14 of each sorted entry
-  __shared__ uint32_t s_ch[kChunkMaxNb + 1], s_co[kChunkMaxNb + 1];
-  __shared__ uint32_t s_w[BS / 64];
-  static_assert(CH <= (1 << 14) && kChunkMaxNb < BS && kChunkMaxNb < (1u << 18), "layout");
-  const uint64_t nflows = c.batch->flow_total;
-  if (count_mode(c, nflows) != 1 || !chunk_scatter(c, nflows) || c.chunk != (uint32_t)CH) return;
-  constexpr uint32_t kCountBlock = BS;  // (the loops below are per workgroup thread)
-  constexpr uint32_t kChunk = CH;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);  // spare bucket: nb
-  const uint64_t n_acc = c.batch->n_acc;
-  const uint64_t nchunks = (n_acc + kChunk - 1) / kChunk;
-  // Barriers per chunk: rank | scan (2) | offsets | placed | read | ids. The counts
-  // are zeroed right after the scan has read them (before three more barriers), so a
-  // workgroup's waves may run into the next chunk's loads and ranks while others
-  // still store this chunk's ids (nothing those touch is reused before the next
-  // rank barrier)
-  for (uint32_t b = tid; b <= nb; b += kCountBlock) s_ch[b] = 0;
-  __syncthreads();
-  // packed K1 -> K3 words: the next chunk's words are loaded while this chunk's
-  // sorted entries are read and its ids stored (one workgroup per CU: nothing else
-  // hides that load)
-  uint32_t nxt[PACK ? U : 1];
-  auto prefetch = [&](uint64_t qn) {
-    if constexpr (PACK) {
-      const uint64_t b0 = qn * kChunk;
-#pragma unroll
-      for (int k = 0; k < U; ++k) {
-        const uint64_t p = b0 + (uint64_t)k * kCountBlock + tid;
-        nxt[k] = qn < nchunks && p < n_acc ? __builtin_nontemporal_load(&c.acc_flow[p]) : 0xFFFFFFFFu;
-      }
-    }
-  };
-  prefetch(blockIdx.x);
-  const uint32_t lmax = 0xFFFFFFFFu >> c.pack_bits;
-  for (uint64_t q = blockIdx.x; q < nchunks; q += gridDim.x) {
-    const uint64_t base = q * kChunk;
-    const uint64_t hi = base + kChunk < n_acc ? base + kChunk : n_acc;
-    const uint32_t nval = (uint32_t)(hi - base);
-    uint32_t ent[U], bk[U], lp[U];
-    if constexpr (PACK) {
-#pragma unroll
-      for (int k = 0; k < U; ++k) {
-        const uint32_t v = nxt[k];
-        const uint32_t cl = v == 0xFFFFFFFFu ? v : (v & ((1u << c.pack_bits) - 1u));
-        uint32_t len = v == 0xFFFFFFFFu ? 0u : v >> c.pack_bits;
-        if (len == lmax) len = c.acc_len[base + (uint64_t)k * kCountBlock + tid];  // saturated
-        const bool big = len >= kRegLenEsc;
-        bk[k] = cl != 0xFFFFFFFFu ? (cl >> kBucketBits) : nb;
-        ent[k] = (cl & (kBucket - 1u)) | ((big ? 0u : len) << kBucketBits);
-        if (big && cl != 0xFFFFFFFFu)
-          atomicAdd((unsigned long long*)&c.cnt[2ull * c.cmap[cl] + 1], (unsigned long long)len);
-      }
-    } else
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {  // two halves of U / 2 loads (register pressure)
-      constexpr int H = U / 2;
-      uint32_t cl[H], len[H];
-      load_acc<H, PACK, BS>(c, base + (uint64_t)h * H * kCountBlock + tid, base, hi, cl, len);
-#pragma unroll
-      for (int k = 0; k < H; ++k) {
-        const bool big = len[k] >= kRegLenEsc;
-        bk[h * H + k] = cl[k] != 0xFFFFFFFFu ? (cl[k] >> kBucketBits) : nb;
-        ent[h * H + k] = (cl[k] & (kBucket - 1u)) | ((big ? 0u : len[k]) << kBucketBits);
-        if (big && cl[k] != 0xFFFFFFFFu)
-          atomicAdd((unsigned long long*)&c.cnt[2ull * c.cmap[cl[k]] + 1], (unsigned long long)len[k]);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const bool valid = (uint32_t)k * kCountBlock + tid < nval;
-      const uint32_t b0 = __builtin_amdgcn_readfirstlane(bk[k]);
-      const uint64_t vm = __ballot(valid);
-      if (__all(!valid || bk[k] == b0)) {
-        // one add for the wave (a hot flow's bucket): ranks in lane order
-        uint32_t r0 = 0;
-        if (lane == 0 && vm) r0 = atomicAdd(&s_ch[b0], (uint32_t)__popcll(vm));
-        r0 = __shfl(r0, 0);
-        lp[k] = r0 + (uint32_t)__popcll(vm & lanemask_lt());
-      } else {
-        lp[k] = valid ? atomicAdd(&s_ch[bk[k]], 1u) : 0u;
-      }
-    }
-    __syncthreads();
-    {
-      uint32_t tot;
-      const uint32_t off = block1024_excl_scan<BS>(tid <= nb ? s_ch[tid] : 0u, s_w, tot);
-      if (tid <= nb) s_co[tid] = off;
-      if (tid <= nb) c.coffs[q * (kChunkMaxNb + 1) + tid] = off;  // [nb] = end of the real buckets
-      if (tid <= nb) s_ch[tid] = 0;  // read by the scan only: zero for the next chunk
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const uint32_t pos = (uint32_t)k * kCountBlock + tid;
-      if (pos >= nval) continue;
-      const uint32_t idx = s_co[bk[k]] + lp[k];
-      s_ent[idx] = ent[k];
-      s_pb[idx] = pos | (bk[k] << 14);
-    }
-    __syncthreads();
-    prefetch(q + gridDim.x);
-    uint32_t id[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const uint32_t idx = (uint32_t)k * kCountBlock + tid;
-      id[k] = 0xFFFFFFFFu;
-      if (idx >= nval) continue;
-      const uint32_t e = s_ent[idx], b = s_pb[idx] >> 14;
-      if (b < nb) {
-        c.region[base + idx] = e;  // consecutive lanes, consecutive entries
-        id[k] = c.omap[(b << kBucketBits) | (e & (kBucket - 1u))];
-      }
-    }
-    __syncthreads();  // every sorted entry read: s_ent becomes the id array
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const uint32_t idx = (uint32_t)k * kCountBlock + tid;
-      if (idx < nval) s_ent[s_pb[idx] & (kChunk - 1u)] = id[k];
-    }
-    __syncthreads();
-    if (c.out_id) {
-#pragma unroll
-      for (int k = 0; k < U; ++k) {
-        const uint64_t p = base + (uint64_t)k * kCountBlock + tid;
-        if (p < hi && p < c.out_cap) __builtin_nontemporal_store(s_ent[(uint32_t)k * kCountBlock + tid], &c.out_id[p]);
-      }
-    }
-  }
-}
-
-// k_count_chunk in 76 KiB of LDS, so TWO workgroups share a CU and one's barrier
-// waits hide under the other's loads and gathers (round 3; k_count_chunk needs
-// 132 KiB and ran latency-bound at 2.5 TB/s, one workgroup per CU). Per chunk of
-// U * BS = 12288 records:
+// 76 KiB of LDS, so TWO workgroups share a CU and one's barrier waits hide under the
+// other's loads and gathers (round 3; round 2's 16384-record form needed 132 KiB and
+// ran latency-bound at 2.5 TB/s, one workgroup per CU; 1024 x 12 and three 8192-record
+// workgroups per CU were slower too). Per chunk:
 //  s_rw[pos]  = claim | min(caplen, kLenSat) << 21 of the record at chunk position
 //               pos (claims < 510 * 4096 < 2^21 wherever the chunked mode runs;
 //               ~0 = no flow); after the gather, the record's output id
 //  s_pos[idx] = the chunk position of bucket-sorted entry idx (u16)
-// 6 B per record instead of 8. The sorted walk reads s_pos[idx] -> s_rw[pos], stores
-// the region entry at region[chunk + idx] and the id back into s_rw[pos] — a slot
-// only its own reader touches, so no barrier between the gather and the write-back.
+// 6 B per record. The sorted walk reads s_pos[idx] -> s_rw[pos], stores the region
+// entry at region[chunk + idx] and the id back into s_rw[pos] — a slot only its own
+// reader touches, so no barrier between the gather and the write-back.
 constexpr uint32_t kLenSat = 2047;  // caplens >= kLenSat are re-read from the K1 scratch
-// CABL (timing-only ablations, variants build; 0 in product launches): 1 no claim -> id
-// gather (id = claim), 2 no region stores, 4 no id stores
-template <bool PACK, int BS, int U, int WG_PER_CU = 2, int CABL = 0>
-// (WG_PER_CU workgroups of BS / 64 waves on a CU's 4 SIMDs)
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WG_PER_CU * BS / 256, 8)))
+template <bool PACK>
+__global__ __launch_bounds__(kChunkBlock) __attribute__((amdgpu_waves_per_eu(2 * kChunkBlock / 256, 8)))
 void k_count_chunk2(CountArgs c) {
-  constexpr int CH = U * BS;
+  constexpr int BS = kChunkBlock, U = kChunk / kChunkBlock, CH = kChunk;
   __shared__ uint32_t s_rw[CH];
   __shared__ uint16_t s_pos[CH];
   __shared__ uint32_t s_ch[kChunkMaxNb + 1], s_co[kChunkMaxNb + 1];
@@ -2213,7 +1580,7 @@ void k_count_chunk2(CountArgs c) {
   static_assert(CH <= (1 << 16) && kChunkMaxNb < BS && (uint64_t)kChunkMaxNb * kBucket < (1u << 21),
                 "layout");
   const uint64_t nflows = c.batch->flow_total;
-  if (count_mode(c, nflows) != 1 || !chunk_scatter(c, nflows) || c.chunk != (uint32_t)CH) return;
+  if (count_mode(c, nflows) != 1 || !chunk_scatter(c, nflows)) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);  // spare bucket: nb
   const uint64_t n_acc = c.batch->n_acc;
@@ -2231,14 +1598,12 @@ void k_count_chunk2(CountArgs c) {
     // workgroups share a CU)
     const uint32_t* af = c.acc_flow + base;
     const uint32_t* al = c.acc_len + base;
-    if (kK3LoadPrio) __builtin_amdgcn_s_setprio(kK3LoadPrio);
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const uint32_t pos = (uint32_t)k * BS + tid;
       w[k] = __builtin_nontemporal_load(&af[pos < nval ? pos : 0u]);
       if (!PACK) lp[k] = __builtin_nontemporal_load(&al[pos < nval ? pos : 0u]);  // (lp: len)
     }
-    if (kK3LoadPrio) __builtin_amdgcn_s_setprio(0);
     // decode: claim | min(caplen, kLenSat) << 21 (~0: no flow). A caplen of
     // >= kLenSat (2047 B: never on an IMIX trace) is rare: the wave then redoes its
     // words with the full value (the side array when the packed field saturated) and
@@ -2322,14 +1687,13 @@ void k_count_chunk2(CountArgs c) {
             l = al[pos];
           }
         }
-        if (!(CABL & 2)) rg[idx] = (cl & (kBucket - 1u)) | l << kBucketBits;  // coalesced runs
-        else asm volatile("" ::"v"(l));
-        id = (CABL & 1) ? cl : c.omap[cl];  // one bucket's 16 KiB window per wave: L1-local
+        rg[idx] = (cl & (kBucket - 1u)) | l << kBucketBits;  // coalesced runs
+        id = c.omap[cl];  // one bucket's 16 KiB window per wave
       }
       s_rw[pos] = id;  // only this thread reads or writes slot pos in this phase
     }
     __syncthreads();
-    if (c.out_id && base < c.out_cap && !(CABL & 4)) {
+    if (c.out_id && base < c.out_cap) {
       uint32_t* oi = c.out_id + base;
       const uint32_t lim = c.out_cap - base < nval ? (uint32_t)(c.out_cap - base) : nval;
 #pragma unroll
@@ -2356,10 +1720,10 @@ __global__ __launch_bounds__(kCountBlock) void k_count_bucket(CountArgs c, uint3
   for (uint32_t t = tid; t < kBucket; t += kCountBlock) s_pk[t] = s_by[t] = 0;
   __syncthreads();
   const uint64_t n_acc = c.batch->n_acc;
-  // segments: the two-pass scatter's g1 blocks, or k_count_chunk's chunks
+  // segments: the two-pass scatter's g1 blocks, or k_count_chunk2's chunks
   const bool chunked = chunk_scatter(c, nflows);
-  const uint64_t per = chunked ? (uint64_t)c.chunk : count_per(n_acc, g1);
-  const uint64_t G = chunked ? (n_acc + c.chunk - 1) / c.chunk : g1;
+  const uint64_t per = chunked ? (uint64_t)kChunk : count_per(n_acc, g1);
+  const uint64_t G = chunked ? (n_acc + kChunk - 1) / kChunk : g1;
   const uint32_t* obase = chunked ? c.coffs : c.offs;
   const uint64_t ostride = chunked ? kChunkMaxNb + 1 : c.nb_max + 1;
   constexpr uint32_t kWaves = kCountBlock / 64;
@@ -2609,559 +1973,6 @@ __global__ void k_finalize(BatchState* b, PersistState* p, uint64_t out_cap, uin
 }
 
 // ---------------------------------------------------------------------------
-// flow-table export / multi-table merge / id remap (multi-GPU row of DESIGN.md §7)
-// An entry is tcbee_flow_entry viewed as u64[8]: key k0..k4, pkts, bytes, first_seen.
-// ---------------------------------------------------------------------------
-__global__ void k_export(FlowTable t, uint64_t* out, uint64_t cap, const PersistState* p,
-                         uint64_t* n_out) {
-  const uint64_t nflows = p->flow_count;
-  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nflows;
-       c += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t* m = t.ent + 8 * c;  // key m[0..4]
-    const uint64_t id = t.cmap[c];
-    if (id >= cap) continue;
-    uint64_t* e = out + 8 * id;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) e[j] = m[j];
-    e[5] = t.cnt[2 * id];
-    e[6] = t.cnt[2 * id + 1];
-    e[7] = t.cfs[c];
-  }
-  if (n_out && blockIdx.x == 0 && threadIdx.x == 0) {
-    n_out[0] = nflows < cap ? nflows : cap;
-    n_out[1] = p->rec_base;  // accepted frames so far = records of this segment
-  }
-}
-
-// Global-order export (flow-hash shards). The table holds the flows of ONE batch
-// (records [rec_base - n_acc, rec_base) of the context); a flow's first record r
-// is mapped to its frame (rec_frame[r], or r itself when every frame of the batch
-// was accepted) and that frame to its position in the global trace. A first
-// record that cannot be placed flags kStShard and exports first_seen ~0.
-__device__ __forceinline__ uint64_t place_first(const GlobalExportArgs& g, uint64_t fs, uint64_t lo,
-                                                uint64_t hi, bool bad_batch) {
-  if (fs >= lo && fs < hi && fs - lo < g.out_cap && !bad_batch) {
-    const uint64_t r = fs - lo;
-    const uint64_t fr = g.rec_frame == nullptr ? r : g.rec_frame[r];
-    if (fr < g.n_frames) return g.frame_gidx[fr];
-  }
-  return ~0ull;
-}
-
-__global__ void k_export_global(GlobalExportArgs g) {
-  const uint64_t nacc = g.batch->n_acc;
-  const uint64_t lo = g.persist->rec_base - nacc;  // advanced by K2
-  const uint64_t hi = lo + nacc;
-  const uint64_t nflows = g.persist->flow_count;
-  const bool bad_batch = g.rec_frame == nullptr && nacc != g.n_frames;
-  bool bad = false;
-  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nflows;
-       c += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t* m = g.tab.ent + 8 * c;
-    const uint64_t id = g.tab.cmap[c];
-    if (id >= g.cap) continue;
-    uint64_t* e = g.out + 8 * id;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) e[j] = m[j];
-    e[5] = g.tab.cnt[2 * id];
-    e[6] = g.tab.cnt[2 * id + 1];
-    const uint64_t gfs = place_first(g, g.tab.cfs[c], lo, hi, bad_batch);
-    bad = bad || gfs == ~0ull;
-    e[7] = gfs;
-  }
-  if (__any(bad) && __lane_id() == 0) atomicOr(&g.persist->status, kStShard);
-  if (g.n_out && blockIdx.x == 0 && threadIdx.x == 0) {
-    g.n_out[0] = nflows < g.cap ? nflows : g.cap;
-    g.n_out[1] = 0;  // first_seen is already global: the merge rebases nothing
-    if (bad_batch) atomicOr(&g.persist->status, kStShard);
-  }
-}
-
-// Records of this rank below each merged flow's first frame: a binary search
-// over the rank's record stream, whose global frame indices ascend.
-__global__ void k_records_before(FlowTable t, const PersistState* p, const uint32_t* rec_frame,
-                                 const uint64_t* frame_gidx, const uint64_t* n_rec_dev,
-                                 uint64_t n_rec_max, uint64_t* out, uint64_t cap) {
-  const uint64_t nflows = p->flow_count;
-  const uint64_t n = n_rec_dev && *n_rec_dev < n_rec_max ? *n_rec_dev : n_rec_max;
-  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nflows;
-       c += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t id = t.cmap[c];
-    if (id >= cap) continue;
-    const uint64_t G = t.cfs[c];
-    uint64_t lo = 0, len = n;  // first record whose global frame >= G
-    while (len > 0) {
-      const uint64_t half = len >> 1, mid = lo + half;
-      const uint64_t gm = frame_gidx[rec_frame ? rec_frame[mid] : mid];
-      if (gm < G) {
-        lo = mid + 1;
-        len -= half + 1;
-      } else {
-        len = half;
-      }
-    }
-    out[id] = lo;
-  }
-}
-
-__global__ void k_set_first_seen(FlowTable t, const PersistState* p, const uint64_t* fs_by_id,
-                                 uint64_t cap) {
-  const uint64_t nflows = p->flow_count;
-  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nflows;
-       c += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t id = t.cmap[c];
-    if (id < cap) t.cfs[c] = fs_by_id[id];
-  }
-}
-
-// Flow-hash exchange (disjoint per-rank tables): for the flows FIRST
-// SEEN IN THIS BATCH (local ids [fbase, fbase + n_new)), the global frame index of
-// each one's first record (placed as k_export_global places it) at out[id - fbase];
-// n_out = {n_new, fbase}. Batches are windows of one global trace (the same global
-// frame range on every rank), so the flows new in a window are exactly the union
-// of every rank's new flows, and older flows keep the ids they already have. The
-// batch's new flows are its claims [fbase, fbase + n_new) (ids a permutation of them).
-__global__ void k_first_frames(GlobalExportArgs g) {
-  const uint64_t nacc = g.batch->n_acc;
-  const uint64_t lo = g.persist->rec_base - nacc;  // advanced by K2
-  const uint64_t hi = lo + nacc;
-  const uint64_t nnew = g.batch->n_new;
-  const uint64_t fbase = g.persist->flow_count - nnew;
-  const bool bad_batch = g.rec_frame == nullptr && nacc != g.n_frames;
-  bool bad = false;
-  for (uint64_t c = fbase + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < fbase + nnew;
-       c += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t id = g.tab.cmap[c];
-    if (id < fbase || id - fbase >= g.cap) continue;
-    const uint64_t gfs = place_first(g, g.tab.cfs[c], lo, hi, bad_batch);
-    bad = bad || gfs == ~0ull;
-    g.out[id - fbase] = gfs;
-  }
-  if (__any(bad) && __lane_id() == 0) atomicOr(&g.persist->status, kStShard);
-  if (g.n_out && blockIdx.x == 0 && threadIdx.x == 0) {
-    g.n_out[0] = nnew < g.cap ? nnew : g.cap;
-    g.n_out[1] = fbase;
-    if (bad_batch || nnew > g.cap) atomicOr(&g.persist->status, kStShard);
-  }
-}
-
-// gid[fbase_r + l] = gbase + l + (this window's new flows of the other ranks whose
-// first frame comes earlier): each rank's array is ascending (its new flows are in
-// local first-seen order, a subsequence of the global order; frames are distinct
-// across ranks), so one binary search per other rank counts them. gbase = global
-// flows of earlier windows; gbase_out = gbase + every rank's new flows.
-__global__ void k_global_ids(const uint64_t* allG, const uint64_t* alln, uint64_t nstride,
-                             uint32_t world, uint32_t rank, uint64_t stride, uint32_t* gid,
-                             uint64_t cap, const uint64_t* gbase_in, uint64_t* gbase_out) {
-  const uint64_t gbase = gbase_in ? *gbase_in : 0;
-  const uint64_t mine = alln[nstride * rank] < stride ? alln[nstride * rank] : stride;
-  const uint64_t fb = alln[nstride * rank + 1];
-  if (gbase_out && blockIdx.x == 0 && threadIdx.x == 0) {
-    uint64_t tot = gbase;
-    for (uint32_t r = 0; r < world; ++r) tot += alln[nstride * r];
-    *gbase_out = tot;
-  }
-  for (uint64_t l = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; l < mine;
-       l += (uint64_t)gridDim.x * blockDim.x) {
-    if (fb + l >= cap) break;
-    const uint64_t G = allG[(uint64_t)rank * stride + l];
-    uint64_t id = gbase + l;
-    for (uint32_t r = 0; r < world; ++r) {
-      if (r == rank) continue;
-      const uint64_t* A = allG + (uint64_t)r * stride;
-      uint64_t lo = 0, len = alln[nstride * r] < stride ? alln[nstride * r] : stride;
-      while (len > 0) {
-        const uint64_t half = len >> 1;
-        if (A[lo + half] < G) {
-          lo += half + 1;
-          len -= half + 1;
-        } else {
-          len = half;
-        }
-      }
-      id += lo;
-    }
-    gid[fb + l] = (uint32_t)id;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Owner exchange (contiguous shards): every rank may hold every
-// flow, so each flow is merged at ONE owner rank, owner = fold32(flow_hash64(key))
-// % world (the NIC-RSS function of tcbee_flowhash_owner), instead of every rank
-// merging every table.
-// ---------------------------------------------------------------------------
-// The local table's flows bucketed by owner: per block, LDS counts per owner, one
-// device-scope reservation per (block, owner), then the entries at their places.
-__global__ __launch_bounds__(kBlock) void k_owner_bucket(OwnerArgs a) {
-  __shared__ uint32_t s_cnt[kMaxOwners];
-  __shared__ uint64_t s_base[kMaxOwners];
-  const uint32_t tid = threadIdx.x;
-  const uint64_t nflows = a.persist->flow_count;
-  if (tid < a.world) s_cnt[tid] = 0;
-  if (blockIdx.x == 0 && tid == 0) a.meta[a.world] = a.persist->rec_base;
-  __syncthreads();
-  uint32_t own[kOwnerItems], rank[kOwnerItems];
-  const uint64_t s0 = (uint64_t)blockIdx.x * kBlock * kOwnerItems + tid;
-  uint32_t dropped = 0;
-#pragma unroll
-  for (int k = 0; k < kOwnerItems; ++k) {
-    own[k] = 0xFFFFFFFFu;
-    const uint64_t c = s0 + (uint64_t)k * kBlock;  // claim
-    if (c >= nflows) continue;
-    const uint64_t* m = a.tab.ent + 8 * c;
-    // a flow whose local id has no place in the id map takes NO segment slot (a
-    // counted but unwritten slot would reach its owner as a phantom flow)
-    if (a.tab.cmap[c] >= a.map_cap) {
-      ++dropped;
-      continue;
-    }
-    own[k] = fold32(flow_hash64(m[0], m[1], m[2], m[3], m[4])) % a.world;
-    rank[k] = atomicAdd(&s_cnt[own[k]], 1u);
-  }
-  __syncthreads();
-  if (tid < a.world) {
-    const uint32_t c = s_cnt[tid];
-    s_base[tid] = c ? atomicAdd((unsigned long long*)&a.meta[tid], (unsigned long long)c) : 0ull;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kOwnerItems; ++k) {
-    if (own[k] == 0xFFFFFFFFu) continue;
-    const uint64_t pos = s_base[own[k]] + rank[k];
-    const uint64_t c = s0 + (uint64_t)k * kBlock;
-    const uint64_t* m = a.tab.ent + 8 * c;
-    if (pos >= a.seg_cap) {  // positions [0, seg_cap) of every segment stay dense
-      ++dropped;
-      continue;
-    }
-    const uint64_t e = (uint64_t)own[k] * a.seg_cap + pos;
-    uint64_t* out = a.ent + 8 * e;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) out[j] = m[j];
-    out[5] = 0;  // pkts / bytes: K3 has not run (the ids come first)
-    out[6] = 0;
-    out[7] = a.tab.cfs[c];  // first_seen, local to this rank's record stream
-    a.lid[e] = a.tab.cmap[c];
-  }
-  // meta[world + 1]: entries this rank dropped. Every rank sees it after the meta
-  // all-gather, so the PEERS of an overflowing rank can flag their ids as wrong too
-  // (tcbee_status_raise_device), not only the rank that dropped them
-  for (int o = 32; o > 0; o >>= 1) dropped += __shfl_xor(dropped, o);
-  if (dropped && __lane_id() == 0) {
-    atomicOr(a.status, kStShard);
-    atomicAdd((unsigned long long*)&a.meta[a.world + 1], (unsigned long long)dropped);
-  }
-}
-
-// status |= kStShard when any v[i * stride] (i < n) is non-zero: a peer's dropped
-// owner entries (OwnerExchange) make this rank's global ids unreliable as well
-__global__ void k_status_raise(const uint64_t* v, uint64_t n, uint64_t stride, uint32_t* status) {
-  bool any = false;
-  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) any |= v[i * stride] != 0;
-  if (__any(any) && __lane_id() == 0) atomicOr(status, kStShard);
-}
-
-__global__ void k_first_seen(FlowTable t, const PersistState* p, uint64_t* out, uint64_t cap,
-                             uint64_t* n_out) {
-  const uint64_t nflows = p->flow_count;
-  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nflows;
-       c += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t id = t.cmap[c];
-    if (id < cap) out[id] = t.cfs[c];
-  }
-  if (n_out && blockIdx.x == 0 && threadIdx.x == 0) {
-    n_out[0] = p->flow_count < cap ? p->flow_count : cap;
-    n_out[1] = 0;
-  }
-}
-
-__global__ void k_owner_return(const uint32_t* ids, const uint64_t* seg_meta, uint32_t world,
-                               uint64_t seg_cap, const uint32_t* gmap, uint64_t gmap_len,
-                               uint32_t* ret) {
-  const uint64_t total = (uint64_t)world * seg_cap;
-  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
-       e += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t r = e / seg_cap, j = e - r * seg_cap;
-    if (j >= seg_meta[2 * r]) continue;
-    const uint32_t id = ids[e];
-    ret[e] = id < gmap_len ? gmap[id] : 0xFFFFFFFFu;
-  }
-}
-
-__global__ void k_owner_apply(const uint32_t* back, const uint32_t* lid, const uint64_t* meta,
-                              uint32_t world, uint64_t seg_cap, uint32_t* map, uint64_t map_cap) {
-  const uint64_t total = (uint64_t)world * seg_cap;
-  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
-       e += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t o = e / seg_cap, j = e - o * seg_cap;
-    if (j >= meta[o]) continue;
-    const uint32_t l = lid[e];
-    if (l < map_cap) map[l] = back[e];
-  }
-}
-
-// omap[claim] = id_map[cmap[claim]] for this batch's flows (output ids of K3)
-__global__ void k_compose(const uint32_t* cmap, const uint32_t* id_map, uint64_t map_len,
-                          const BatchState* b, uint32_t* omap) {
-  const uint64_t n = b->flow_total;
-  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < n;
-       c += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t l = cmap[c];
-    omap[c] = l < map_len ? id_map[l] : 0xFFFFFFFFu;
-  }
-}
-
-// Inserts every valid entry of nseg segments (segment r = rank r's local table,
-// first_seen local to that rank) with first_seen rebased to the global record
-// index; per-slot counters summed. out_slot[e] = merged slot (or ~0).
-__global__ void k_merge_insert(MergeArgs g) {
-  const uint64_t total = g.nseg * g.stride;
-  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
-       e += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t seg = e / g.stride, j = e % g.stride;
-    if (j >= g.seg_meta[2 * seg]) {
-      g.out_slot[e] = 0xFFFFFFFFu;
-      continue;
-    }
-    const uint64_t* E = g.ent + 8 * e;
-    const uint64_t K[5] = {E[0], E[1], E[2], E[3], E[4]};
-    uint32_t fs = 0xFFFFFFFFu, claim = 0xFFFFFFFFu;
-    // (a fresh table: every claim is new, fbase 0)
-    const uint32_t s = flow_upsert(g.tab, K, flow_hash64(K[0], K[1], K[2], K[3], K[4]), g.batch,
-                                   g.new_list, g.persist, 0, fs, claim);
-    g.out_slot[e] = s == 0xFFFFFFFFu ? 0xFFFFFFFFu : claim;
-    if (s == 0xFFFFFFFFu) continue;
-    atomicAdd((unsigned long long*)&g.mcnt[2ull * claim], (unsigned long long)E[5]);
-    atomicAdd((unsigned long long*)&g.mcnt[2ull * claim + 1], (unsigned long long)E[6]);
-    uint64_t base = 0;  // records of the segments before this one
-    for (uint64_t q = 0; q < seg; ++q) base += g.seg_meta[2 * q + 1];
-    // the slot's fs32 (max_total_records < 2^31, checked by the ABI); an unplaceable
-    // first_seen (~0 from a flagged exporter) stays past every record of the merge
-    const uint64_t gfs = base + E[7];
-    atomicMin(slot_fs_any(g.tab, s), gfs < (uint64_t)kFs32Flag ? (uint32_t)gfs : kFs32Flag - 1u);
-  }
-}
-
-// entry slot -> merged dense id; per-slot counters -> by-id counters; flow count
-__global__ void k_merge_finish(MergeArgs g) {
-  const uint64_t total = g.nseg * g.stride;
-  const uint64_t nflows = g.batch->n_new;  // a fresh table: claims [0, n_new)
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  for (uint64_t e = t0; e < total; e += stride) {
-    const uint32_t c = g.out_slot[e];
-    g.out_slot[e] = c == 0xFFFFFFFFu || c >= nflows ? 0xFFFFFFFFu : g.tab.cmap[c];
-  }
-  for (uint64_t c = t0; c < nflows; c += stride) {
-    const uint64_t id = g.tab.cmap[c];
-    g.tab.cnt[2 * id] = g.mcnt[2 * c];
-    g.tab.cnt[2 * id + 1] = g.mcnt[2 * c + 1];
-  }
-  for (uint64_t w = t0; w <= g.batch->fs_max_word; w += stride) g.bitmap[w] = 0;
-  if (t0 == 0) {
-    uint64_t recs = 0;
-    for (uint64_t q = 0; q < g.nseg; ++q) recs += g.seg_meta[2 * q + 1];
-    g.persist->flow_count += g.batch->n_new;
-    g.persist->rec_base += recs;
-  }
-}
-
-// ids[p] = map[ids[p]] (N>1 local -> global flow ids). The first kRemapLds map
-// entries are staged in LDS as u16 (a rank's local ids are dense from 0; a global
-// id >= 0xFFFF is looked up in HBM instead), 32 KiB per workgroup, so the remap
-// that overlaps the next step's K1 takes few of K1's LDS slots; the ids stream
-// through as 16-B non-temporal vectors, 4 per thread in flight.
-constexpr uint32_t kRemapLds = 16384;
-constexpr int kRemapBlock = 512;
-__global__ __launch_bounds__(kRemapBlock) void k_remap(uint32_t* ids, uint64_t n_max,
-                                                       const uint64_t* n_dev, const uint32_t* map,
-                                                       uint64_t map_len) {
-  __shared__ uint16_t s_map[kRemapLds];
-  const uint64_t n = n_dev && *n_dev < n_max ? *n_dev : n_max;
-  const uint32_t m = map_len < kRemapLds ? (uint32_t)map_len : kRemapLds;
-  for (uint32_t j = threadIdx.x; j < m; j += kRemapBlock) {
-    const uint32_t g = map[j];
-    s_map[j] = g < 0xFFFFu ? (uint16_t)g : (uint16_t)0xFFFFu;
-  }
-  __syncthreads();
-  auto tr = [&](uint32_t v) -> uint32_t {
-    if (v < m) {
-      const uint32_t g = s_map[v];
-      return g != 0xFFFFu ? g : map[v];
-    }
-    return v < map_len ? map[v] : 0xFFFFFFFFu;
-  };
-  const uint64_t t0 = blockIdx.x * (uint64_t)kRemapBlock + threadIdx.x;
-  const uint64_t stride = (uint64_t)gridDim.x * kRemapBlock;
-  uint64_t head = ((16u - ((uintptr_t)ids & 15u)) & 15u) >> 2;  // scalar up to 16-B alignment
-  if (head > n) head = n;
-  for (uint64_t p = t0; p < head; p += stride) ids[p] = tr(ids[p]);
-  u32x4* v4 = reinterpret_cast<u32x4*>(ids + head);
-  const uint64_t n4 = (n - head) >> 2;
-  constexpr int R = 4;
-  for (uint64_t q0 = t0; q0 < n4; q0 += stride * R) {
-    u32x4 v[R];
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      const uint64_t q = q0 + (uint64_t)u * stride;
-      v[u] = __builtin_nontemporal_load(v4 + (q < n4 ? q : n4 - 1));  // unconditional loads
-    }
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      const uint64_t q = q0 + (uint64_t)u * stride;
-      if (q < n4) {
-        u32x4 o;
-        o[0] = tr(v[u][0]);
-        o[1] = tr(v[u][1]);
-        o[2] = tr(v[u][2]);
-        o[3] = tr(v[u][3]);
-        __builtin_nontemporal_store(o, v4 + q);
-      }
-    }
-  }
-  for (uint64_t p = head + (n4 << 2) + t0; p < n; p += stride) ids[p] = tr(ids[p]);
-}
-
-// ---------------------------------------------------------------------------
-// synthetic trace headers (payload stays as the caller zeroed it)
-// ---------------------------------------------------------------------------
-__global__ void k_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
-                      uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed,
-                      const uint64_t* gidx, const uint64_t* zcdf) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    uint8_t h[kGenHdrMax];
-    gen_header(h, gidx ? gidx[i] : first_index + i, len[i], kind, n_flows, seed, zcdf);
-    const uint32_t hl = gen_header_len(kind);
-    const uint32_t m = len[i] < hl ? len[i] : hl;
-    uint8_t* dst = arena + off[i];
-    for (uint32_t b = 0; b < m; ++b) dst[b] = h[b];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// flow-hash shard of the synthetic trace (config 4: the NIC-RSS view of 8 GPUs)
-// ---------------------------------------------------------------------------
-// caplen of global frame i (== tcbee_amd.trace.synth_index)
-__device__ __forceinline__ uint32_t gen_caplen(uint64_t i, int imix, uint64_t seed) {
-  if (!imix) return 64u;
-  const uint64_t r = splitmix64((seed ^ 0x1A1Eull) + i) % 12u;
-  return r < 7 ? 64u : (r < 11 ? 576u : 1500u);
-}
-// the flow hash of global frame i (the IpTuple K1 builds for this IPv4/TCP frame,
-// xdp.rs:116-127) folded to 32 bits
-__device__ __forceinline__ uint32_t gen_fold(const ShardArgs& a, uint64_t i) {
-  const GenFields g = gen_fields(i, a.kind, a.n_flows, a.seed);
-  const uint64_t k1 = (uint64_t)bswap32(g.saddr) << 32, k3 = (uint64_t)bswap32(g.daddr) << 32;
-  const uint64_t k4 = (uint64_t)g.sport | ((uint64_t)g.dport << 16) | ((uint64_t)kTcpProtocol << 32);
-  return fold32(flow_hash64(0, k1, 0, k3, k4));
-}
-// owner GPU of global frame i: the folded hash mod world, or through the RSS
-// indirection table (a NIC's receive-side scaling: hash bucket -> queue)
-__device__ __forceinline__ uint32_t gen_owner(const ShardArgs& a, uint64_t i) {
-  const uint32_t h = gen_fold(a, i);
-  return a.rss ? (uint32_t)a.rss[h % a.rss_len] : h % a.world;
-}
-
-__device__ __forceinline__ uint32_t shard_mine(const ShardArgs& a, uint64_t i0, uint32_t& bits) {
-  bits = 0;
-#pragma unroll 4
-  for (int k = 0; k < kShardPer; ++k) {
-    const uint64_t i = i0 + k;
-    if (i < a.n_global && gen_owner(a, i) == a.rank) bits |= 1u << k;
-  }
-  return (uint32_t)__popc(bits);
-}
-
-__global__ __launch_bounds__(kBlock) void k_shard_count(ShardArgs a) {
-  __shared__ uint32_t s_tmp[4];
-  uint32_t bits;
-  const uint32_t c = shard_mine(a, blockIdx.x * kShardChunk + threadIdx.x * (uint64_t)kShardPer, bits);
-  uint32_t total;
-  (void)block_excl_scan(c, s_tmp, total);
-  if (threadIdx.x == 0) a.scratch[blockIdx.x] = total;
-}
-
-// one block: exclusive prefix over the chunk counts (each thread a contiguous run)
-__global__ __launch_bounds__(kBlock) void k_shard_scan(ShardArgs a, uint64_t nchunks) {
-  __shared__ uint64_t s_sum[kBlock];
-  __shared__ uint32_t s_bad;
-  const uint64_t per = (nchunks + kBlock - 1) / kBlock;
-  const uint64_t lo = threadIdx.x * per, hi = lo + per < nchunks ? lo + per : nchunks;
-  uint64_t sum = 0;
-  for (uint64_t b = lo; b < hi; ++b) sum += a.scratch[b];
-  s_sum[threadIdx.x] = sum;
-  if (threadIdx.x == 0) s_bad = 0;
-  __syncthreads();
-  // an RSS entry >= world would drop its bucket's frames on every rank: such a
-  // table yields the count ~0 (TCBEE_RSS_INVALID), which no shard can have
-  if (a.rss)
-    for (uint32_t b = threadIdx.x; b < a.rss_len; b += kBlock)
-      if ((uint32_t)a.rss[b] >= (uint32_t)a.world) s_bad = 1;
-  __syncthreads();
-  uint64_t base = 0;
-  for (uint32_t t = 0; t < threadIdx.x; ++t) base += s_sum[t];
-  for (uint64_t b = lo; b < hi; ++b) {
-    const uint64_t c = a.scratch[b];
-    a.scratch[b] = base;
-    base += c;
-  }
-  if (threadIdx.x == kBlock - 1) *a.n_out = s_bad ? ~0ull : base;
-}
-
-__global__ __launch_bounds__(kBlock) void k_shard_write(ShardArgs a) {
-  __shared__ uint32_t s_tmp[4];
-  const uint64_t i0 = blockIdx.x * kShardChunk + threadIdx.x * (uint64_t)kShardPer;
-  uint32_t bits;
-  const uint32_t c = shard_mine(a, i0, bits);
-  uint32_t total;
-  uint64_t pos = a.scratch[blockIdx.x] + block_excl_scan(c, s_tmp, total);
-  while (bits) {
-    const int k = __ffs(bits) - 1;
-    bits &= bits - 1;
-    if (pos < a.cap) {
-      a.gidx[pos] = i0 + k;
-      a.caplen[pos] = gen_caplen(i0 + k, a.imix, a.seed);
-    }
-    ++pos;
-  }
-}
-
-// frames per RSS bucket: an LDS histogram per block, one device add per bucket
-__global__ __launch_bounds__(kBlock) void k_rss_load(ShardArgs a) {
-  __shared__ uint32_t s_h[kRssMaxLen];
-  for (uint32_t b = threadIdx.x; b < a.rss_len; b += kBlock) s_h[b] = 0;
-  __syncthreads();
-  for (uint64_t i = blockIdx.x * (uint64_t)kBlock + threadIdx.x; i < a.n_global;
-       i += (uint64_t)gridDim.x * kBlock)
-    atomicAdd(&s_h[gen_fold(a, a.first + i) % a.rss_len], 1u);
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < a.rss_len; b += kBlock)
-    if (s_h[b]) atomicAdd((unsigned long long*)&a.scratch[b], (unsigned long long)s_h[b]);
-}
-
-hipError_t launch_rss_load(const ShardArgs& a, hipStream_t s) {
-  const hipError_t e = hipMemsetAsync(a.scratch, 0, sizeof(uint64_t) * a.rss_len, s);
-  if (e != hipSuccess) return e;
-  if (a.n_global == 0) return hipSuccess;
-  // a block covers >= 64k frames (its histogram flush costs rss_len adds)
-  uint64_t g = (a.n_global + 65535) / 65536;
-  if (g > 2048) g = 2048;
-  hipLaunchKernelGGL(k_rss_load, dim3((unsigned)g), dim3(kBlock), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_shard_index(const ShardArgs& a, hipStream_t s) {
-  const uint64_t nchunks = (a.n_global + kShardChunk - 1) / kShardChunk;
-  if (nchunks == 0) return hipMemsetAsync(a.n_out, 0, sizeof(uint64_t), s);
-  hipLaunchKernelGGL(k_shard_count, dim3((unsigned)nchunks), dim3(kBlock), 0, s, a);
-  hipLaunchKernelGGL(k_shard_scan, dim3(1), dim3(kBlock), 0, s, a, nchunks);
-  hipLaunchKernelGGL(k_shard_write, dim3((unsigned)nchunks), dim3(kBlock), 0, s, a);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 static unsigned grid_for(uint64_t n, unsigned cap = 4096) {
@@ -3174,98 +1985,22 @@ hipError_t launch_table_init(FlowTable t, hipStream_t s) {
   return hipGetLastError();
 }
 
-#if TCBEE_VARIANTS
-// k1v (TCBEE_K1V at context creation) and the TCBEE_PROBE_AUX / TCBEE_ABLATE /
-// TCBEE_STAGE / TCBEE_NT environment: staging, occupancy, cache-policy A/B variants
-// and timing-only ablations (several write wrong records on purpose), read at every
-// launch (a process may switch them between contexts). Returns true when it
-// launched a variant.
 template <int FPL>
-static bool launch_parse_variant(const ParseArgs& a, bool flows, hipStream_t s, int k1v, dim3 grid) {
-  if constexpr (FPL == 2) if (flows && k1v) {
-    switch (k1v) {
-      case 1: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 0>), grid, dim3(kBlock), 0, s, a); return true;
-      case 2: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 5>), grid, dim3(kBlock), 0, s, a); return true;
-      case 3: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1, false, 6>), grid, dim3(kBlock), 0, s, a); return true;
-      // 512-thread tiles (1024 frames): half the tiles and look-back hops (the
-      // context sizes ntiles for it: k1_tile_blocks)
-      case 20: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 0, false, 0, 0, 512>), grid, dim3(512), 0, s, a); return true;
-#define TCBEE_HPOL_CASE(P) \
-      case 10 + P: hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 0, false, 0, P>), grid, dim3(kBlock), 0, s, a); return true;
-      TCBEE_HPOL_CASE(1) TCBEE_HPOL_CASE(2) TCBEE_HPOL_CASE(3) TCBEE_HPOL_CASE(4) TCBEE_HPOL_CASE(5)
-      TCBEE_HPOL_CASE(6)
-#undef TCBEE_HPOL_CASE
-      default: return false;
-    }
-  }
-  const int aux = [] {
-    const char* e = getenv("TCBEE_PROBE_AUX");
-    return e ? atoi(e) : kAuxPlain;
-  }();
-  const int abl = [] {
-    const char* e = getenv("TCBEE_ABLATE");
-    return e ? atoi(e) : 0;
-  }();
-  if (FPL == 2 && abl) {
-#define TCBEE_ABL_CASE(B)                                                                      \
-  case B:                                                                                      \
-    if (flows) hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, B>), grid, dim3(kBlock), 0, s, a); \
-    else hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain, B>), grid, dim3(kBlock), 0, s, a);     \
-    return true;
-    switch (abl) {
-      TCBEE_ABL_CASE(1) TCBEE_ABL_CASE(2) TCBEE_ABL_CASE(4) TCBEE_ABL_CASE(8)
-      TCBEE_ABL_CASE(16) TCBEE_ABL_CASE(3) TCBEE_ABL_CASE(31) TCBEE_ABL_CASE(32) TCBEE_ABL_CASE(96)
-      TCBEE_ABL_CASE(224) TCBEE_ABL_CASE(352) TCBEE_ABL_CASE(480)
-      default: break;
-    }
-#undef TCBEE_ABL_CASE
-  }
-  const int stage = [] {
-    const char* e = getenv("TCBEE_STAGE");
-    return e ? atoi(e) : 0;
-  }();
-  if (stage == 1) {
-    if (flows) hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 1>), grid, dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain, 0, 1>), grid, dim3(kBlock), 0, s, a);
-    return true;
-  }
-  const int nt = [] {
-    const char* e = getenv("TCBEE_NT");
-    return e ? atoi(e) : 0;
-  }();
-  if (nt) {
-    if (flows) hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain, 0, 0, true>), grid, dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain, 0, 0, true>), grid, dim3(kBlock), 0, s, a);
-    return true;
-  }
-  if (flows && aux == kAuxSc1) {
-    hipLaunchKernelGGL((k_parse<FPL, true, kAuxSc1>), grid, dim3(kBlock), 0, s, a);
-    return true;
-  }
-  return false;
-}
-#endif
-
-template <int FPL>
-static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s, int k1v) {
+static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s) {
   const dim3 grid((unsigned)a.ntiles);
-#if TCBEE_VARIANTS
-  // timing-only ablations and A/B variants: the variants build only
-  // (libtcbee_amd_variants.so); the product library has no such dispatch
-  if (launch_parse_variant<FPL>(a, flows, s, k1v, grid)) return hipGetLastError();
-#else
-  (void)k1v;
-#endif
-  if (flows) hipLaunchKernelGGL((k_parse<FPL, true, kAuxPlain>), grid, dim3(kBlock), 0, s, a);
-  else hipLaunchKernelGGL((k_parse<FPL, false, kAuxPlain>), grid, dim3(kBlock), 0, s, a);
+  if (flows) hipLaunchKernelGGL((k_parse<FPL, true>), grid, dim3(kBlock), 0, s, a);
+  else hipLaunchKernelGGL((k_parse<FPL, false>), grid, dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s, int k1v) {
+hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s) {
+  // (FPL 2 in every product context; 1 and 4: test tilings of the variants build)
   switch (fpl) {
-    case 1: return launch_parse_fpl<1>(a, flows, s, k1v);
-    case 2: return launch_parse_fpl<2>(a, flows, s, k1v);
-    case 4: return launch_parse_fpl<4>(a, flows, s, k1v);
+    case 2: return launch_parse_fpl<2>(a, flows, s);
+#if TCBEE_VARIANTS
+    case 1: return launch_parse_fpl<1>(a, flows, s);
+    case 4: return launch_parse_fpl<4>(a, flows, s);
+#endif
     default: return hipErrorInvalidValue;
   }
 }
@@ -3293,116 +2028,18 @@ hipError_t launch_rank(const RankArgs& r, hipStream_t s) {
   return hipGetLastError();
 }
 
-#if TCBEE_VARIANTS
-static void launch_count_variant(const CountArgs& c, unsigned g1, unsigned g1s, unsigned g2,
-                                 hipStream_t s, int k3v) {
-  const dim3 grid(g1);
-  // k3v (TCBEE_K3ABL at context creation): timing-only ablation / tiling A/B
-#define KC(U, A)                                                                     \
-  do {                                                                               \
-    if (c.pack_bits) hipLaunchKernelGGL((k_count<U, A, true>), grid, dim3(kCountBlock), 0, s, c); \
-    else hipLaunchKernelGGL((k_count<U, A, false>), grid, dim3(kCountBlock), 0, s, c);            \
-  } while (0)
-  switch (k3v) {
-    case 1: KC(8, 1); break;
-    case 2: KC(8, 2); break;
-    case 4: KC(8, 4); break;
-    case 7: KC(8, 7); break;
-    case 16: KC(16, 0); break;
-    case 8: KC(8, 8); break;    // plain id stores (A/B)
-    case 24: KC(16, 8); break;  // 16 records per lane, plain id stores (A/B)
-    case 32: KC(4, 0); break;
-    case 40:  // 16-B loads of four packed words per lane: U = 4 / 2 loads per lane
-    case 42:  // (U = 8 spills 328 VGPRs)
-      if (c.pack_bits && k3v == 40) hipLaunchKernelGGL((k_count<4, 0, true, true>), grid, dim3(kCountBlock), 0, s, c);
-      else if (c.pack_bits) hipLaunchKernelGGL((k_count<2, 0, true, true>), grid, dim3(kCountBlock), 0, s, c);
-      else KC(8, 0);
-      break;
-    default:
-      if (c.wide_iter) KC(16, 0);
-      else KC(8, 0);
-      break;
-  }
-#undef KC
-  // the two-pass scatter only where the chunked one may not cover a batch (tables
-  // of >= kChunkMaxNb buckets, or the A/B hook): no empty launches otherwise
-  const bool two_pass = !c.coffs || c.chunk_off || c.nb_max >= kChunkMaxNb;
-  if (g2 && two_pass) {
-    const dim3 gs(g1s);
-    switch (k3v) {  // 64 + SABL: timing-only scatter ablations
-      case 65: hipLaunchKernelGGL((k_count_scatter<8, false, 1>), gs, dim3(kCountBlock), 0, s, c); break;
-      case 66: hipLaunchKernelGGL((k_count_scatter<8, false, 2>), gs, dim3(kCountBlock), 0, s, c); break;
-      case 68: hipLaunchKernelGGL((k_count_scatter<8, false, 4>), gs, dim3(kCountBlock), 0, s, c); break;
-      case 70: hipLaunchKernelGGL((k_count_scatter<8, false, 6>), gs, dim3(kCountBlock), 0, s, c); break;
-      case 80: hipLaunchKernelGGL((k_count_scatter<16, false, 0>), gs, dim3(kCountBlock), 0, s, c); break;
-      case 74: hipLaunchKernelGGL((k_count_scatter<8, false, 10>), gs, dim3(kCountBlock), 0, s, c); break;
-      case 78: hipLaunchKernelGGL((k_count_scatter<8, false, 14>), gs, dim3(kCountBlock), 0, s, c); break;
-      default:
-        if (c.pack_bits) hipLaunchKernelGGL((k_count_scatter<8, true>), gs, dim3(kCountBlock), 0, s, c);
-        else hipLaunchKernelGGL((k_count_scatter<8, false>), gs, dim3(kCountBlock), 0, s, c);
-    }
-    // (each of the three returns at once unless the batch's bucket count is its own)
-    if (c.pack_bits) hipLaunchKernelGGL((k_count_scatter_staged<4, true>), gs, dim3(kCountBlock), 0, s, c);
-    else hipLaunchKernelGGL((k_count_scatter_staged<4, false>), gs, dim3(kCountBlock), 0, s, c);
-  }
-  if (g2) {
-    if (c.coffs && c.chunk == 8u * 1024u && k3v == 95) {  // 52 KiB: three workgroups per CU (A/B)
-      const dim3 gc(g1s ? (g1s * 3 + 1) / 2 : 1);
-      if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk2<true, 512, 16, 3>), gc, dim3(512), 0, s, c);
-      else hipLaunchKernelGGL((k_count_chunk2<false, 512, 16, 3>), gc, dim3(512), 0, s, c);
-    } else if (c.coffs && c.chunk == 12u * 1024u) {  // 76 KiB of LDS: two workgroups per CU
-      const dim3 gc(g1s ? g1s : 1);
-      // 512-thread workgroups, 24 records per thread (TCBEE_K3ABL=94: 1024 x 12, A/B):
-      // 125M records, 125k flows (packed words): 470 vs 476 us; 1M flows (unpacked):
-      // 705 vs 827 us (round 2's k_count_chunk: 607 / 868 us; profiles/r03_k3ab_*)
-      if (k3v == 94) {
-        if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk2<true, 1024, 12>), gc, dim3(1024), 0, s, c);
-        else hipLaunchKernelGGL((k_count_chunk2<false, 1024, 12>), gc, dim3(1024), 0, s, c);
-      } else if (k3v >= 101 && k3v <= 107 && c.pack_bits) {  // 100 + CABL: timing-only ablations
-#define TCBEE_CABL_CASE(A) \
-        case 100 + A: hipLaunchKernelGGL((k_count_chunk2<true, 512, 24, 2, A>), gc, dim3(512), 0, s, c); break;
-        switch (k3v) {
-          TCBEE_CABL_CASE(1) TCBEE_CABL_CASE(2) TCBEE_CABL_CASE(3) TCBEE_CABL_CASE(4) TCBEE_CABL_CASE(5)
-          TCBEE_CABL_CASE(6) TCBEE_CABL_CASE(7)
-        }
-#undef TCBEE_CABL_CASE
-      } else {
-        if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk2<true, 512, 24>), gc, dim3(512), 0, s, c);
-        else hipLaunchKernelGGL((k_count_chunk2<false, 512, 24>), gc, dim3(512), 0, s, c);
-      }
-    } else if (c.coffs && c.chunk == 16u * 1024u) {  // 132 KiB of LDS: one workgroup per CU
-      const dim3 gc((g1s + 1) / 2);
-      if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk<true, 1024>), gc, dim3(1024), 0, s, c);
-      else hipLaunchKernelGGL((k_count_chunk<false, 1024>), gc, dim3(1024), 0, s, c);
-    } else if (c.coffs) {  // 8192-record chunks, 68 KiB: two workgroups per CU
-      const dim3 gc(g1s ? g1s : 1);
-      if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk<true, 512>), gc, dim3(512), 0, s, c);
-      else hipLaunchKernelGGL((k_count_chunk<false, 512>), gc, dim3(512), 0, s, c);
-    }
-    hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1s);
-  }
-}
-#endif
-
-hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned g2, hipStream_t s,
-                        int k3v) {
-#if TCBEE_VARIANTS
-  // k3v (TCBEE_K3ABL at context creation): timing-only ablations / tiling A/B —
-  // the variants build only
-  launch_count_variant(c, g1, g1s, g2, s, k3v);
-#else
-  (void)k3v;
+hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned g2, hipStream_t s) {
   const dim3 grid(g1);
   if (c.wide_iter) {  // large batches: 16 records per lane and iteration
-    if (c.pack_bits) hipLaunchKernelGGL((k_count<16, 0, true>), grid, dim3(kCountBlock), 0, s, c);
-    else hipLaunchKernelGGL((k_count<16, 0, false>), grid, dim3(kCountBlock), 0, s, c);
+    if (c.pack_bits) hipLaunchKernelGGL((k_count<16, true>), grid, dim3(kCountBlock), 0, s, c);
+    else hipLaunchKernelGGL((k_count<16, false>), grid, dim3(kCountBlock), 0, s, c);
   } else {
-    if (c.pack_bits) hipLaunchKernelGGL((k_count<8, 0, true>), grid, dim3(kCountBlock), 0, s, c);
-    else hipLaunchKernelGGL((k_count<8, 0, false>), grid, dim3(kCountBlock), 0, s, c);
+    if (c.pack_bits) hipLaunchKernelGGL((k_count<8, true>), grid, dim3(kCountBlock), 0, s, c);
+    else hipLaunchKernelGGL((k_count<8, false>), grid, dim3(kCountBlock), 0, s, c);
   }
-  // the two-pass scatter only where the chunked one may not cover a batch (tables
-  // of >= kChunkMaxNb buckets): no empty launches otherwise
-  const bool two_pass = !c.coffs || c.nb_max >= kChunkMaxNb;
+  // the two-pass scatter only where the chunked one may not cover a batch (tables of
+  // >= kChunkMaxNb buckets, or the test hook): no empty launches otherwise
+  const bool two_pass = !c.coffs || c.chunk_off || c.nb_max >= kChunkMaxNb;
   if (g2 && two_pass) {
     const dim3 gs(g1s);
     // (each of the two returns at once unless the batch's bucket count is its own)
@@ -3416,14 +2053,13 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
   }
   if (g2) {
     if (c.coffs) {
-      // 12288-record chunks in 76 KiB of LDS: two 512-thread workgroups per CU
+      // kChunk-record chunks in 76 KiB of LDS: two 512-thread workgroups per CU
       const dim3 gc(g1s ? g1s : 1);
-      if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk2<true, 512, 24>), gc, dim3(512), 0, s, c);
-      else hipLaunchKernelGGL((k_count_chunk2<false, 512, 24>), gc, dim3(512), 0, s, c);
+      if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk2<true>), gc, dim3(kChunkBlock), 0, s, c);
+      else hipLaunchKernelGGL((k_count_chunk2<false>), gc, dim3(kChunkBlock), 0, s, c);
     }
     hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1s);
   }
-#endif
   // mode 0 needs kCountBins threads; mode 1 up to nb_max * kBucket (grid-stride)
   // (1024-thread blocks: mode 0 takes 64 claims per block, its 16 waves split the rows)
   const unsigned gr = (g2 || c.range_ok) ? 256u : (unsigned)(kCountBins / 256);
@@ -3436,127 +2072,6 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
 hipError_t launch_finalize(BatchState* b, PersistState* p, uint64_t out_cap, uint64_t* out_n,
                            tcbee_counters* ctr, int direction, hipStream_t s) {
   hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1), 0, s, b, p, out_cap, out_n, ctr, direction);
-  return hipGetLastError();
-}
-
-hipError_t launch_export(FlowTable t, uint64_t* out, uint64_t cap, const PersistState* p,
-                         uint64_t* n_out, hipStream_t s) {
-  hipLaunchKernelGGL(k_export, dim3(grid_for(t.max_claims)), dim3(kBlock), 0, s, t, out, cap, p, n_out);
-  return hipGetLastError();
-}
-
-hipError_t launch_export_global(const GlobalExportArgs& g, hipStream_t s) {
-  hipLaunchKernelGGL(k_export_global, dim3(grid_for(g.tab.max_claims)), dim3(kBlock), 0, s, g);
-  return hipGetLastError();
-}
-
-hipError_t launch_records_before(FlowTable t, const PersistState* p, const uint32_t* rec_frame,
-                                 const uint64_t* frame_gidx, const uint64_t* n_rec,
-                                 uint64_t n_rec_max, uint64_t* out, uint64_t cap, hipStream_t s) {
-  hipLaunchKernelGGL(k_records_before, dim3(grid_for(t.max_claims)), dim3(kBlock), 0, s, t, p,
-                     rec_frame, frame_gidx, n_rec, n_rec_max, out, cap);
-  return hipGetLastError();
-}
-
-hipError_t launch_set_first_seen(FlowTable t, const PersistState* p, const uint64_t* fs_by_id,
-                                 uint64_t cap, hipStream_t s) {
-  hipLaunchKernelGGL(k_set_first_seen, dim3(grid_for(t.max_claims)), dim3(kBlock), 0, s, t, p,
-                     fs_by_id, cap);
-  return hipGetLastError();
-}
-
-hipError_t launch_owner_bucket(const OwnerArgs& a, hipStream_t s) {
-  const uint64_t per = (uint64_t)kBlock * kOwnerItems;
-  const uint64_t nb = (a.tab.max_claims + per - 1) / per;
-  hipLaunchKernelGGL(k_owner_bucket, dim3((unsigned)nb), dim3(kBlock), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_status_raise(const uint64_t* v, uint64_t n, uint64_t stride, uint32_t* status,
-                               hipStream_t s) {
-  hipLaunchKernelGGL(k_status_raise, dim3(1), dim3(kBlock), 0, s, v, n, stride, status);
-  return hipGetLastError();
-}
-
-hipError_t launch_first_seen(FlowTable t, const PersistState* p, uint64_t* out, uint64_t cap,
-                             uint64_t* n_out, hipStream_t s) {
-  hipLaunchKernelGGL(k_first_seen, dim3(grid_for(t.max_claims)), dim3(kBlock), 0, s, t, p, out, cap,
-                     n_out);
-  return hipGetLastError();
-}
-
-hipError_t launch_owner_return(const uint32_t* ids, const uint64_t* seg_meta, uint32_t world,
-                               uint64_t seg_cap, const uint32_t* gmap, uint64_t gmap_len,
-                               uint32_t* ret, hipStream_t s) {
-  hipLaunchKernelGGL(k_owner_return, dim3(grid_for((uint64_t)world * seg_cap)), dim3(kBlock), 0, s,
-                     ids, seg_meta, world, seg_cap, gmap, gmap_len, ret);
-  return hipGetLastError();
-}
-
-hipError_t launch_owner_apply(const uint32_t* back, const uint32_t* lid, const uint64_t* meta,
-                              uint32_t world, uint64_t seg_cap, uint32_t* map, uint64_t map_cap,
-                              hipStream_t s) {
-  hipLaunchKernelGGL(k_owner_apply, dim3(grid_for((uint64_t)world * seg_cap)), dim3(kBlock), 0, s,
-                     back, lid, meta, world, seg_cap, map, map_cap);
-  return hipGetLastError();
-}
-
-hipError_t launch_first_frames(const GlobalExportArgs& g, hipStream_t s) {
-  hipLaunchKernelGGL(k_first_frames, dim3(grid_for(g.tab.max_claims)), dim3(kBlock), 0, s, g);
-  return hipGetLastError();
-}
-
-hipError_t launch_global_ids(const uint64_t* allG, const uint64_t* alln, uint64_t nstride,
-                             uint32_t world, uint32_t rank, uint64_t stride, uint32_t* gid,
-                             uint64_t cap, const uint64_t* gbase_in, uint64_t* gbase_out,
-                             hipStream_t s) {
-  hipLaunchKernelGGL(k_global_ids, dim3(grid_for(stride)), dim3(kBlock), 0, s, allG, alln, nstride,
-                     world, rank, stride, gid, cap, gbase_in, gbase_out);
-  return hipGetLastError();
-}
-
-hipError_t launch_compose(const uint32_t* cmap, const uint32_t* id_map, uint64_t map_len,
-                          const BatchState* b, uint32_t* omap, uint64_t max_flows, hipStream_t s) {
-  hipLaunchKernelGGL(k_compose, dim3(grid_for(max_flows)), dim3(kBlock), 0, s, cmap, id_map, map_len,
-                     b, omap);
-  return hipGetLastError();
-}
-
-hipError_t launch_merge(const MergeArgs& g, const RankArgs& r, hipStream_t s) {
-  const unsigned grid = grid_for(g.nseg * g.stride);
-  hipLaunchKernelGGL(k_merge_insert, dim3(grid), dim3(kBlock), 0, s, g);
-  hipError_t e = launch_rank(r, s);
-  if (e != hipSuccess) return e;
-  const uint64_t work = g.nseg * g.stride > g.tab.max_claims ? g.nseg * g.stride : g.tab.max_claims;
-  hipLaunchKernelGGL(k_merge_finish, dim3(grid_for(work)), dim3(kBlock), 0, s, g);
-  return hipGetLastError();
-}
-
-hipError_t launch_remap(uint32_t* ids, uint64_t n_max, const uint64_t* n_dev, const uint32_t* map,
-                        uint64_t map_len, hipStream_t s) {
-  // up to 512 workgroups (beside the next step's K1, 32..512 workgroups gave the
-  // same step time once the LDS map was u16: TCBEE_REMAP_GRID, variants build)
-#if TCBEE_VARIANTS
-  static const uint64_t gmax = [] {
-    const char* e = getenv("TCBEE_REMAP_GRID");
-    const long long v = e ? atoll(e) : 0;
-    return v > 0 ? (uint64_t)v : 512ull;  // unset, 0 or garbage: the default
-  }();
-#else
-  constexpr uint64_t gmax = 512;
-#endif
-  const uint64_t want = (n_max + 4ull * kRemapBlock - 1) / (4ull * kRemapBlock);
-  hipLaunchKernelGGL(k_remap, dim3((unsigned)(want < gmax ? (want ? want : 1) : gmax)),
-                     dim3(kRemapBlock), 0, s, ids, n_max, n_dev, map,
-                     map_len);
-  return hipGetLastError();
-}
-
-hipError_t launch_gen(uint8_t* arena, const uint64_t* off, const uint32_t* len, uint64_t n,
-                      uint64_t first_index, int kind, uint64_t n_flows, uint64_t seed,
-                      hipStream_t s, const uint64_t* gidx, const uint64_t* zcdf) {
-  hipLaunchKernelGGL(k_gen, dim3(grid_for(n, 8192)), dim3(kBlock), 0, s, arena, off, len, n,
-                     first_index, kind, n_flows, seed, gidx, zcdf);
   return hipGetLastError();
 }
 

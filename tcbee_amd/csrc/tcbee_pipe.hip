@@ -188,6 +188,8 @@ struct tcbee_pipe {
   uint8_t* reg_rec = nullptr;
   uint32_t* reg_id = nullptr;
   uint64_t reg_cap = 0;
+  bool own_rec = false, own_id = false;  // page-locked by this pipe (else borrowed:
+                                         // already registered when it was handed in)
   uint64_t prefetch = 48;  // header-window gather: frames ahead (TCBEE_PIPE_PF, 0 = off)
   int nt_copy = 1;         // header-window gather: fixed-size 16-B loads + streaming
                            // stores into the staging (TCBEE_PIPE_NT=0: memcpy)
@@ -196,11 +198,25 @@ struct tcbee_pipe {
 namespace {
 
 void unregister_output(tcbee_pipe* p) {
-  if (p->reg_rec) (void)hipHostUnregister(p->reg_rec);
-  if (p->reg_id) (void)hipHostUnregister(p->reg_id);
+  if (p->reg_rec && p->own_rec) (void)hipHostUnregister(p->reg_rec);
+  if (p->reg_id && p->own_id) (void)hipHostUnregister(p->reg_id);
   p->reg_rec = nullptr;
   p->reg_id = nullptr;
   p->reg_cap = 0;
+  p->own_rec = p->own_id = false;
+}
+
+// hipHostRegister, or nothing when the range is page-locked already (by another
+// pipe or by the caller): then it is borrowed and left registered on release
+hipError_t register_range(void* ptr, uint64_t bytes, bool& own) {
+  const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
+  if (e == hipErrorHostMemoryAlreadyRegistered) {
+    (void)hipGetLastError();  // (clear the sticky-free error state)
+    own = false;
+    return hipSuccess;
+  }
+  own = e == hipSuccess;
+  return e;
 }
 
 void free_pipe(tcbee_pipe* p) {
@@ -432,8 +448,8 @@ int tcbee_pipe_create(tcbee_pipe** out, int device, const tcbee_pipe_cfg* pc,
   p->device = device;
   p->cfg = c;
 #if TCBEE_VARIANTS
-  // gather prefetch distance / streaming copies (A/B, variants build only)
-  if (const char* e = std::getenv("TCBEE_PIPE_PF")) p->prefetch = std::strtoull(e, nullptr, 10);
+  // test hook (variants build only): TCBEE_PIPE_NT=0 gathers with memcpy instead of
+  // streaming stores
   if (const char* e = std::getenv("TCBEE_PIPE_NT")) p->nt_copy = std::atoi(e);
 #endif
   int rc = tcbee_ctx_create(&p->ctx, device, c.chunk_frames, 0, max_flows ? max_flows : 1 << 20);
@@ -448,13 +464,9 @@ int tcbee_pipe_create(tcbee_pipe** out, int device, const tcbee_pipe_cfg* pc,
   try {
     p->slots.resize(c.depth);
     // `threads` in all: with staged outputs a quarter copy records out while the
-    // rest gather (TCBEE_PIPE_CTHREADS: the copy-out share, A/B); with the caller's
-    // arrays registered (direct D2H, nothing to copy out) all of them gather
-    unsigned ct = c.threads >= 4 ? c.threads / 4 : 1;
-#if TCBEE_VARIANTS
-    if (const char* e = std::getenv("TCBEE_PIPE_CTHREADS")) ct = (unsigned)std::atoi(e);
-#endif
-    if (ct < 1) ct = 1;
+    // rest gather; with the caller's arrays registered (direct D2H, nothing to copy
+    // out) all of them gather
+    const unsigned ct = c.threads >= 4 ? c.threads / 4 : 1;
     p->gt_staged = c.threads > ct ? c.threads - ct : 1;
     p->pool = new Pool(c.threads > p->gt_staged ? c.threads : p->gt_staged);
     p->cpool = new Pool(ct);
@@ -474,10 +486,10 @@ int tcbee_pipe_register_output(tcbee_pipe* p, uint8_t* out_rec74, uint64_t cap,
   TRY_HIP(hipStreamSynchronize(p->s_d2h));  // no D2H into the old arrays in flight
   unregister_output(p);
   if (!cap) return TCBEE_OK;
-  TRY_HIP(hipHostRegister(out_rec74, cap * TCBEE_RECORD_BYTES, hipHostRegisterDefault));
+  TRY_HIP(register_range(out_rec74, cap * TCBEE_RECORD_BYTES, p->own_rec));
   p->reg_rec = out_rec74;
   if (out_flow_id) {
-    const hipError_t e = hipHostRegister(out_flow_id, cap * 4, hipHostRegisterDefault);
+    const hipError_t e = register_range(out_flow_id, cap * 4, p->own_id);
     if (e != hipSuccess) {
       unregister_output(p);
       return map_err(e);

@@ -66,11 +66,16 @@ int main(int argc, char** argv) {
   snprintf(out_path, sizeof out_path, "%s%s", prefix, egress ? "tc.tcp" : "xdp.tcp");
 
   const double t0 = now_s();
+  /* every path out of here releases what was opened so far (one exit below) */
   tcbee_pcap* pc = NULL;
-  int rc = tcbee_pcap_open(&pc, pcap_path);
-  if (rc) return fail("pcap_open", rc);
+  tcbee_pipe* pipe = NULL;
+  tcbee_tcpfile* tf = NULL;
+  const char* what = NULL;
+  int rc = 0;
   tcbee_frames fr;
-  if ((rc = tcbee_pcap_frames(pc, &fr))) return fail("pcap_frames", rc);
+  memset(&fr, 0, sizeof fr);
+  if ((rc = tcbee_pcap_open(&pc, pcap_path))) { what = "pcap_open"; goto out; }
+  if ((rc = tcbee_pcap_frames(pc, &fr))) { what = "pcap_frames"; goto out; }
 
   tcbee_pipe_cfg pcfg;
   memset(&pcfg, 0, sizeof pcfg);
@@ -78,13 +83,14 @@ int main(int argc, char** argv) {
   pcfg.window = window;
   pcfg.depth = 4;
   pcfg.threads = threads;
-  tcbee_pipe* pipe = NULL;
-  if ((rc = tcbee_pipe_create(&pipe, 0, &pcfg, 1u << 20))) return fail("pipe_create", rc);
+  if ((rc = tcbee_pipe_create(&pipe, 0, &pcfg, 1u << 20))) { what = "pipe_create"; goto out; }
 
   /* the drain task's writer: create + append, 10000 x 72-B entries buffered
      (handlers/mod.rs:65-139; 74-B entries here, as tcbee-process reads them) */
-  tcbee_tcpfile* tf = NULL;
-  if ((rc = tcbee_tcpfile_open(&tf, out_path, 10000u * TCBEE_RECORD_BYTES))) return fail("tcpfile_open", rc);
+  if ((rc = tcbee_tcpfile_open(&tf, out_path, 10000u * TCBEE_RECORD_BYTES))) {
+    what = "tcpfile_open";
+    goto out;
+  }
 
   tcbee_cfg cfg;
   memset(&cfg, 0, sizeof cfg);
@@ -95,25 +101,30 @@ int main(int argc, char** argv) {
   memset(&ctr, 0, sizeof ctr);
   rc = tcbee_pipe_run(pipe, &fr, &cfg, NULL, 0, NULL, append_chunk, tf, &records, &ctr);
   const int rc_close = tcbee_tcpfile_close(tf);
-  if (rc) return fail("pipe_run", rc);
-  if (rc_close) return fail("tcpfile_close", rc_close);
+  tf = NULL;
+  if (rc) { what = "pipe_run"; goto out; }
+  if ((rc = rc_close)) { what = "tcpfile_close"; goto out; }
 
   tcbee_ctx* ctx = NULL;
   uint64_t flows = 0;
-  if ((rc = tcbee_pipe_ctx(pipe, &ctx)) || (rc = tcbee_flow_count(ctx, &flows)))
-    return fail("flow_count", rc);
-  if ((rc = tcbee_metrics_write(prefix, &ctr, 0, 0))) return fail("metrics_write", rc);
+  if ((rc = tcbee_pipe_ctx(pipe, &ctx)) || (rc = tcbee_flow_count(ctx, &flows))) {
+    what = "flow_count";
+    goto out;
+  }
+  if ((rc = tcbee_metrics_write(prefix, &ctr, 0, 0))) { what = "metrics_write"; goto out; }
   tcbee_sink_stats st;
   memset(&st, 0, sizeof st);
-  if (db && (rc = tcbee_process_files(prefix, db, 0, &st))) return fail("process_files", rc);
+  if (db && (rc = tcbee_process_files(prefix, db, 0, &st))) { what = "process_files"; goto out; }
   const double el = now_s() - t0;
-  tcbee_pipe_destroy(pipe);
-  tcbee_pcap_close(pc);
   printf("{\"frames\": %llu, \"records\": %llu, \"flows\": %llu, \"ingress\": %llu, \"egress\": %llu, "
          "\"handled\": %llu, \"dropped\": %llu, \"db_records\": %llu, \"seconds\": %.6f}\n",
          (unsigned long long)fr.n, (unsigned long long)records, (unsigned long long)flows,
          (unsigned long long)ctr.ingress, (unsigned long long)ctr.egress,
          (unsigned long long)ctr.handled, (unsigned long long)ctr.dropped,
          (unsigned long long)st.records, el);
-  return 0;
+out:
+  if (tf) (void)tcbee_tcpfile_close(tf);
+  if (pipe) tcbee_pipe_destroy(pipe);
+  if (pc) tcbee_pcap_close(pc);
+  return what ? fail(what, rc) : 0;
 }

@@ -44,6 +44,9 @@ class Pipeline:
         self.parser = PacketParser._borrow(ctx, device, chunk_frames, max_flows, self._L)
         self.window = window
         self._registered = None  # (out_rec, out_id) page-locked for direct D2H
+        # "registered" (direct D2H into the registered arrays) or "staged"
+        # (calibrate_output chooses per box)
+        self.output_mode = "staged"
 
     def register_output(self, out_rec, out_id=None) -> None:
         """Page-lock the caller's output arrays once (tcbee_pipe_register_output):
@@ -54,6 +57,7 @@ class Pipeline:
             _lib.check(self._L.tcbee_pipe_register_output(self._h, None, 0, None),
                        "tcbee_pipe_register_output")
             self._registered = None
+            self.output_mode = "staged"
             return
         if (out_rec.dtype != np.uint8 or out_rec.ndim != 2 or out_rec.shape[1] != _lib.RECORD_BYTES
                 or not out_rec.flags.c_contiguous):
@@ -65,6 +69,44 @@ class Pipeline:
                                                       _ptr(out_id)),
                    "tcbee_pipe_register_output")
         self._registered = (out_rec, out_id)
+        self.output_mode = "registered"
+
+    def calibrate_output(self, trace: Trace, frames: int = 4_000_000, reps: int = 2) -> dict:
+        """Choose how this pipe returns records for the caller's registered arrays:
+        straight into them (direct D2H) or through pinned staging + a host copy-out.
+        Which is faster depends on the box's host memory (round 4: 515 vs 343 Mpkt/s on
+        one box, 438 vs 452 on another), so a short calibration on a prefix of `trace`
+        decides: both modes alternate (ABBA order) `reps` times over the first
+        `frames` frames and the faster median is kept — the pipe stays registered, or
+        releases its registration and stages. Returns the timings and the choice
+        (also in self.output_mode). register_output() first."""
+        import time
+        if self._registered is None:
+            raise ValueError("calibrate_output: register_output() first")
+        rec, ids = self._registered
+        m = min(frames, trace.n, len(rec))
+        sub = trace.slice(0, m)
+        ts = {"registered": [], "staged": []}
+        order = ["registered", "staged", "staged", "registered"] * reps
+        for mode in order:
+            if mode == "registered" and self._registered is None:
+                self.register_output(rec, ids)
+            elif mode == "staged" and self._registered is not None:
+                self.register_output(None)
+            self.reset_flows()
+            t0 = time.perf_counter()
+            self.run(sub, out_rec=rec[:m], out_id=None if ids is None else ids[:m])
+            ts[mode].append(time.perf_counter() - t0)
+        med = {k: float(np.median(v)) for k, v in ts.items()}
+        self.output_mode = min(med, key=med.get)
+        if self.output_mode == "registered" and self._registered is None:
+            self.register_output(rec, ids)
+        elif self.output_mode == "staged" and self._registered is not None:
+            self.register_output(None)
+        self.reset_flows()
+        return {"frames": m, "reps": len(order) // 2,
+                "registered_mpkts": round(m / med["registered"] / 1e6, 1),
+                "staged_mpkts": round(m / med["staged"] / 1e6, 1), "chosen": self.output_mode}
 
     def run(self, trace: Trace, filter_port: int = 0, direction: int = _lib.DIR_INGRESS,
             flows: bool = True, collect: bool = True, sink=None, out_rec=None,

@@ -225,26 +225,24 @@ def test_arena_beyond_4GiB(parser, oracle):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("fpl,k1v", [("1", "0"), ("2", "0"), ("4", "0"), ("2", "20")])
-def test_tile_shape_determinism(gpu, oracle, fpl, k1v, monkeypatch):
-    """Same trace, different frames-per-lane tilings (and 512-thread tiles,
-    TCBEE_K1V=20) -> identical outputs."""
+@pytest.mark.parametrize("fpl", ["1", "2", "4"])
+def test_tile_shape_determinism(gpu, oracle, fpl, monkeypatch):
+    """Same trace, different frames-per-lane tilings -> identical outputs."""
     from tracegen import mixed_trace
     monkeypatch.setenv("TCBEE_FPL", fpl)
-    monkeypatch.setenv("TCBEE_K1V", k1v)
     tr = mixed_trace(150_000, seed=77, n_flows=2000)
     with tcbee_amd.PacketParser(max_frames=1 << 18, max_arena=1 << 26, max_flows=1 << 14,
                                 variants=True) as p:
         assert_same(p.parse(tr), oracle.parse(tr), p.flows())
 
 
-@pytest.mark.parametrize("every,k1v", [("1", "0"), ("3", "0"), ("64", "0"), ("3", "20")])
-def test_lookback_recount_fallback(gpu, oracle, every, k1v, monkeypatch):
+@pytest.mark.parametrize("every,fpl", [("1", "2"), ("3", "2"), ("64", "2"), ("3", "4")])
+def test_lookback_recount_fallback(gpu, oracle, every, fpl, monkeypatch):
     """Tiles that never publish force successors to recount them from the input:
     results stay exact (the look-back assumes no dispatch order)."""
     from tracegen import mixed_trace
     monkeypatch.setenv("TCBEE_TEST_WITHHOLD", every)
-    monkeypatch.setenv("TCBEE_K1V", k1v)
+    monkeypatch.setenv("TCBEE_FPL", fpl)
     tr = mixed_trace(20_000 if every == "1" else 60_000, seed=91, n_flows=300)
     with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 25, max_flows=1 << 12,
                                 variants=True) as p:
@@ -525,7 +523,7 @@ def test_k3_range_mode_large_batches(gpu, oracle, pool, n, k3v, monkeypatch):
     >= 16M frames), mode 3 here."""
     import torch
     from tracegen import mixed_trace
-    monkeypatch.setenv("TCBEE_K3ABL", k3v or "0")
+    monkeypatch.setenv("TCBEE_TEST_K3_WIDE", "1" if k3v else "0")
     tr = mixed_trace(n, seed=pool, n_flows=pool)  # ~1.9 distinct keys per pool flow
     ln = tr.caplen.copy()
     rng = np.random.default_rng(7)
@@ -626,20 +624,20 @@ def _concat(a, b):
                  np.concatenate([a.caplen, b.caplen]), np.concatenate([a.ts_ns, b.ts_ns]))
 
 
-@pytest.mark.parametrize("variant", ["0", "0n", "94", "93", "91", "92"])
+@pytest.mark.parametrize("variant", ["0", "0n", "twopass"])
 @pytest.mark.parametrize("flows", [40_000, 150_000])
 def test_k3_chunked_scatter(gpu, oracle, variant, flows, monkeypatch):
     """K3 mode 1's single-pass chunked scatter (k_count_chunk2: chunks of 12288
     records in 76 KiB of LDS, two workgroups per CU — "0n": unpacked K1 -> K3
-    words, 94: 1024-thread workgroups of 12 records each; 93: round 2's k_count_chunk, 16384 records,
-    92: 8192 — bucket-sorted in LDS, ids gathered bucket by bucket, region runs per
-    chunk) and the two-pass scatter it replaced (TCBEE_K3ABL=91), bit-exact vs the
+    words — bucket-sorted in LDS, ids gathered bucket by bucket, region runs per
+    chunk) and the two-pass scatter the product keeps for tables of more than 510
+    buckets ("twopass": TCBEE_TEST_K3_TWOPASS forces it here), bit-exact vs the
     oracle: a ragged last chunk, caplens past the 20-bit region field and the
     packed K1 -> K3 field, a single-flow stretch (every wave on one bucket), two
     batches (claims of batch 1 looked up again in batch 2)."""
     from tracegen import mixed_trace
     monkeypatch.setenv("TCBEE_TEST_K3_NORANGE", "1")
-    monkeypatch.setenv("TCBEE_K3ABL", variant.rstrip("n"))
+    monkeypatch.setenv("TCBEE_TEST_K3_TWOPASS", "1" if variant == "twopass" else "0")
     if variant.endswith("n"):
         monkeypatch.setenv("TCBEE_TEST_NOPACK", "1")
     mt = mixed_trace(350_001, seed=123, n_flows=flows)
@@ -738,30 +736,27 @@ def test_small_context_big_frames_over_k3_blocks(gpu, oracle, monkeypatch, fuse)
 
 
 def test_product_library_ignores_variant_env(gpu, oracle, monkeypatch):
-    """the product library reads no environment variable. With the
-    ablation / test-hook variables set (ABLATE=8 replaces frame offsets by i*64,
-    K3ABL=1 skips the pkts/bytes bins, NOPACK/WITHHOLD/NO_FUSE_RANK select test
-    paths), a product context still matches the oracle bit-exact, while a context of
-    the variants build does follow them (its records differ) — so the setting took."""
+    """the product library reads no environment variable. With every
+    test-hook variable of the variants build set (NORANGE/TWOPASS/NOBUCKET select
+    other K3 modes, NOPACK/WITHHOLD/NO_FUSE_RANK/WIDE/FPL/WALK other K1-K3 paths), a
+    product context keeps its own paths (K3 mode 3 on a ~19k-flow trace) and matches
+    the oracle bit-exact, while a context of the variants build does follow them (it
+    reports K3 mode 2: the setting took) and matches the oracle too."""
     from tracegen import mixed_trace
-    for k, v in {"TCBEE_ABLATE": "8", "TCBEE_K3ABL": "1", "TCBEE_TEST_NOPACK": "1",
-                 "TCBEE_TEST_WITHHOLD": "3", "TCBEE_NO_FUSE_RANK": "1", "TCBEE_K1V": "20",
-                 "TCBEE_FPL": "4", "TCBEE_TEST_K3_NORANGE": "1", "TCBEE_STAGE": "1",
-                 "TCBEE_NT": "1", "TCBEE_PROBE_AUX": "16", "TCBEE_WALK": "0"}.items():
+    for k, v in {"TCBEE_TEST_NOPACK": "1", "TCBEE_TEST_WITHHOLD": "3",
+                 "TCBEE_NO_FUSE_RANK": "1", "TCBEE_FPL": "4", "TCBEE_TEST_K3_NORANGE": "1",
+                 "TCBEE_TEST_K3_NOBUCKET": "1", "TCBEE_TEST_K3_TWOPASS": "1",
+                 "TCBEE_TEST_K3_WIDE": "1", "TCBEE_WALK": "0"}.items():
         monkeypatch.setenv(k, v)
-    tr = mixed_trace(120_000, seed=808, n_flows=2000)
+    tr = mixed_trace(300_000, seed=808, n_flows=10_000)
     orc = oracle.parse(tr)
-    with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 26, max_flows=1 << 14) as p:
-        assert_same(p.parse(tr), orc, p.flows())
-        assert p.status() == 0
-    # (the ablation is dispatched for the default tiling only: FPL 2, no K1 variant)
-    monkeypatch.delenv("TCBEE_K1V")
-    monkeypatch.delenv("TCBEE_FPL")
-    with tcbee_amd.PacketParser(max_frames=1 << 17, max_arena=1 << 26, max_flows=1 << 14,
-                                variants=True) as v:
-        res = v.parse(tr)
-        # (frames read at i * 64 instead of their offsets: other frames accepted)
-        assert res.n != len(orc[0]) or not np.array_equal(res.records, orc[0])
+    assert 12_288 < len(orc[4]) < 36_000
+    for variants, mode in ((False, 3), (True, 2)):
+        with tcbee_amd.PacketParser(max_frames=1 << 19, max_arena=1 << 28, max_flows=1 << 16,
+                                    variants=variants) as p:
+            assert_same(p.parse(tr), orc, p.flows())
+            assert p.status() == 0
+            assert p.count_mode() == mode, (variants, p.count_mode())
 
 
 @pytest.mark.parametrize("short", [0, 9])
@@ -798,16 +793,14 @@ def test_max_wide_flows_exact_bound(gpu, oracle, short):
         assert not np.isin(fi[~refused], keys).any()
 
 
-@pytest.mark.parametrize("k3v", ["40", "42", "16"])
 @pytest.mark.parametrize("flows", [1, 40, 5000])
-def test_k3_vector_loads_variant(gpu, oracle, flows, k3v, monkeypatch):
-    """K3 mode 0 with 16-B loads of four packed K1 -> K3 words per lane (variants
-    build, TCBEE_K3ABL=40/42: 4 / 2 loads per lane), and with 16 records per lane and
-    iteration (16: the product's form for batches of >= 16M frames): a ragged tail (scalar fallback),
+def test_k3_wide_iteration_variant(gpu, oracle, flows, monkeypatch):
+    """K3 mode 0 with 16 records per lane and iteration (the product's form for
+    batches of >= 16M frames, forced here by TCBEE_TEST_K3_WIDE): a ragged tail,
     saturated packed caplens (the side array), > 64 KiB frames (device atomics), a
     hot flow (the wave-uniform add) — bit-exact vs the oracle."""
     from tracegen import mixed_trace
-    monkeypatch.setenv("TCBEE_K3ABL", k3v)
+    monkeypatch.setenv("TCBEE_TEST_K3_WIDE", "1")
     tr = mixed_trace(150_001, seed=303, n_flows=flows)
     rng = np.random.default_rng(8)
     big = rng.choice(tr.n, size=300, replace=False)

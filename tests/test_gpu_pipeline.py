@@ -173,6 +173,45 @@ def test_pipeline_registered_output(gpu, oracle, window):
             p.register_output(np.zeros((10, 70), np.uint8))
 
 
+def test_pipeline_shared_registration_and_calibration(gpu, oracle):
+    """Round 5: two pipes share ONE registered output pair
+    (the second borrows the first's page-locking, and releasing the borrower leaves it
+    registered for the owner); calibrate_output times direct D2H against staging on
+    a prefix and keeps the faster; whichever it keeps, records / ids / counters / the
+    table equal the oracle, and forcing the other mode gives the same bytes."""
+    t = mixed_trace(60_000, seed=62, n_flows=500)
+    want = oracle.parse(t)
+    n = len(want[0])
+    out = np.zeros((n, 74), np.uint8)
+    ids = np.zeros(n, np.uint32)
+    with Pipeline(device=0, chunk_frames=4096, window=64, depth=3, threads=4,
+                  max_flows=1 << 12) as owner:
+        owner.register_output(out, ids)
+        with Pipeline(device=0, chunk_frames=4096, window=64, depth=3, threads=4,
+                      max_flows=1 << 12) as b:
+            b.register_output(out, ids)  # already page-locked: borrowed
+            check_same(b.run(t, out_rec=out, out_id=ids), want, b.flows())
+            cal = b.calibrate_output(t, frames=20_000, reps=1)
+            assert cal["chosen"] in ("registered", "staged") and cal["frames"] == 20_000
+            assert b.output_mode == cal["chosen"]
+            assert cal["registered_mpkts"] > 0 and cal["staged_mpkts"] > 0
+            out[:] = 0
+            ids[:] = 0
+            check_same(b.run(t, out_rec=out, out_id=ids), want, b.flows())
+            # the other mode, forced: same bytes
+            if b.output_mode == "registered":
+                b.register_output(None)
+            else:
+                b.register_output(out, ids)
+            b.reset_flows()
+            out[:] = 0
+            check_same(b.run(t, out_rec=out, out_id=ids), want, b.flows())
+        # the borrower is gone: the owner's registration still holds (direct D2H)
+        out[:] = 0
+        ids[:] = 0
+        check_same(owner.run(t, out_rec=out, out_id=ids), want, owner.flows())
+
+
 def test_pipeline_empty_and_tiny(gpu, oracle):
     with Pipeline(device=0, chunk_frames=1024) as p:
         t0 = mixed_trace(0, seed=1)

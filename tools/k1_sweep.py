@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--fpl", default="1,2,4")
     ap.add_argument("--workloads", default="imix10k,imix1,64B1")
-    ap.add_argument("--var", default="", help="extra env A/B, e.g. TCBEE_K3ABL=0,2")
+    ap.add_argument("--var", default="", help="extra env A/B of a variants-build test hook, e.g. TCBEE_TEST_K3_WIDE=0,1")
     ap.add_argument("--flows-only", action="store_true", help="only the flows-on variants")
     ap.add_argument("--cap-mult", default="4", help="max_flows = mult x flows (comma list: A/B)")
     ap.add_argument("--warm", action="store_true", help="keep the flow table across steps (no reset)")
@@ -74,7 +74,7 @@ def main():
         for r in range(args.rounds):
             for v in variants:
                 p = parsers[v]
-                if var_name:  # (the variants build reads TCBEE_ABLATE & co at every launch)
+                if var_name:  # (set again per variant: a hook read at launch sees its own value)
                     os.environ[var_name] = v[2]
                 def step():
                     if not args.warm:

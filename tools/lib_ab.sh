@@ -4,6 +4,8 @@
 # own process on the same box (TCBEE_AB_LIB selects the library; tools only).
 #   tools/lib_ab.sh build [REV]        (here, on the CPU)
 #   tools/lib_ab.sh run REV -- CMD...  (on the GPU box: CMD with the old library)
+# REV "wt:NAME": the working tree as it is now, kept under build/ab_wt_NAME;
+# HIPEXTRA: extra compiler flags for that build (build-time experiment knobs, -D...)
 set -eu
 cd "$(dirname "$0")/.."
 case "${1:-}" in
@@ -11,16 +13,16 @@ case "${1:-}" in
     rev=${2:-HEAD}
     d=build/ab_${rev//:/_}
     rm -rf "$d"; mkdir -p "$d/tcbee_amd/csrc" "$d/include"
-    # REV "wt:NAME": the working tree as it is now, kept under build/ab_wt:NAME
-    for f in tcbee_kernels.hip tcbee_capi.hip tcbee_pipe.hip tcbee_gen.h tcbee_internal.h tcbee_layout.h; do
-      case $rev in wt:*) cp "tcbee_amd/csrc/$f" "$d/tcbee_amd/csrc/$f" ;;
-                   *) git show "$rev:tcbee_amd/csrc/$f" > "$d/tcbee_amd/csrc/$f" ;; esac
-    done
-    case $rev in wt:*) cp include/tcbee_amd.h "$d/include/tcbee_amd.h" ;;
-                 *) git show "$rev:include/tcbee_amd.h" > "$d/include/tcbee_amd.h" ;; esac
-    # HIPEXTRA: extra compiler flags for this build (e.g. -DTCBEE_K1_LOAD_PRIO=3)
+    case $rev in
+      wt:*) cp tcbee_amd/csrc/*.hip tcbee_amd/csrc/*.h "$d/tcbee_amd/csrc/"
+            cp include/tcbee_amd.h "$d/include/tcbee_amd.h" ;;
+      *) for f in $(git ls-tree --name-only "$rev" tcbee_amd/csrc/ | grep -E '\.(hip|h)$'); do
+           git show "$rev:$f" > "$d/$f"
+         done
+         git show "$rev:include/tcbee_amd.h" > "$d/include/tcbee_amd.h" ;;
+    esac
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function ${HIPEXTRA:-} -shared \
-      -o "$d/libtcbee_amd.so" "$d/tcbee_amd/csrc/tcbee_kernels.hip" "$d/tcbee_amd/csrc/tcbee_capi.hip" "$d/tcbee_amd/csrc/tcbee_pipe.hip"
+      -o "$d/libtcbee_amd.so" "$d"/tcbee_amd/csrc/*.hip
     echo "$d/libtcbee_amd.so" ;;
   run)
     rev=$2; shift 3
