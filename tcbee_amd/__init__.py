@@ -11,12 +11,14 @@ from ._lib import (DIR_EGRESS, DIR_INGRESS, EXPORTED, F_NO_FLOWS, KEY_BYTES, LIB
 from .parser import (FLOW_DTYPE, PacketParser, ParseResult, flow_hash64, gen_frames_device,
                      gen_frames_index_device, gen_rss_load_device, gen_shard_index_device,
                      gen_shard_scratch_words)
-from .trace import RSS_BUCKETS, Trace, rss_table, splitmix64, synth_index, synth_trace
+from .trace import (RSS_BUCKETS, Trace, rss_flows_per_rank, rss_table, splitmix64, synth_flow_folds,
+                    synth_index, synth_trace)
 
 __all__ = [
     "DIR_EGRESS", "DIR_INGRESS", "EXPORTED", "F_NO_FLOWS", "KEY_BYTES", "LIB_PATH",
     "RECORD_BYTES", "TcbeeError", "device_count", "lib", "FLOW_DTYPE", "PacketParser",
     "ParseResult", "flow_hash64", "gen_frames_device", "gen_frames_index_device",
     "gen_rss_load_device", "gen_shard_index_device", "gen_shard_scratch_words", "RSS_BUCKETS",
-    "Trace", "rss_table", "splitmix64", "synth_index", "synth_trace",
+    "Trace", "rss_flows_per_rank", "rss_table", "splitmix64", "synth_flow_folds", "synth_index",
+    "synth_trace",
 ]

@@ -120,6 +120,35 @@ def test_flowhash_owner_matches_device_shards():
         assert own[i] == ((h ^ (h >> 32)) & 0xFFFFFFFF) % 4
 
 
+def test_rss_flows_per_rank_matches_the_trace(oracle):
+    """bench.py sizes flow-hash shards from tcbee_amd.rss_flows_per_rank before any
+    frame is parsed: every flow's fold32(flow_hash64(key)) computed from its flow
+    number (synth_flow_folds) equals the oracle's hash of the key the hook builds
+    from that flow's frames, and the per-rank counts equal the distinct flows of
+    each host partitioner shard (modulo placement and an RSS table)."""
+    import tcbee_amd
+    from tcbee_amd import host
+    n_flows = 3000
+    tr = tcbee_amd.synth_trace(60_000, sizes="imix", kind=1, n_flows=n_flows)
+    folds = set(tcbee_amd.synth_flow_folds(n_flows).tolist())
+    keys = {}
+    for i in range(0, tr.n, 7):
+        _, key = oracle.hook(tr.frame(i))
+        h = oracle.flow_hash64(key)
+        keys[key] = (h ^ (h >> 32)) & 0xFFFFFFFF
+    assert len(keys) > 2700 and set(keys.values()) <= folds
+    rng = np.random.default_rng(5)
+    table = rng.integers(0, 3, size=tcbee_amd.RSS_BUCKETS).astype(np.uint16)
+    all_keys = [oracle.hook(tr.frame(i))[1] for i in range(tr.n)]
+    for world, tab in ((4, None), (3, table)):
+        per = tcbee_amd.rss_flows_per_rank(n_flows, world, table=tab)
+        assert per.sum() == n_flows
+        own = host.flowhash_owner(tr, world, threads=2, rss=tab)
+        for r in range(world):
+            # 60k frames of 3000 uniform flows: every flow appears
+            assert len({k for k, o in zip(all_keys, own) if o == r}) == per[r]
+
+
 def test_rss_table_lpt():
     """rss_table: every bucket mapped to a GPU < world, deterministic, and the
     per-GPU load within one bucket of the mean (longest-processing-time greedy)."""
