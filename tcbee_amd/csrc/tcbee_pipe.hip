@@ -200,6 +200,7 @@ namespace {
 void unregister_output(tcbee_pipe* p) {
   if (p->reg_rec && p->own_rec) (void)hipHostUnregister(p->reg_rec);
   if (p->reg_id && p->own_id) (void)hipHostUnregister(p->reg_id);
+  (void)hipGetLastError();  // (a failed release must not surface in a later call)
   p->reg_rec = nullptr;
   p->reg_id = nullptr;
   p->reg_cap = 0;
@@ -207,14 +208,17 @@ void unregister_output(tcbee_pipe* p) {
 }
 
 // hipHostRegister, or nothing when the range is page-locked already (by another
-// pipe or by the caller): then it is borrowed and left registered on release
+// pipe or by the caller): then it is borrowed and left registered on release. (The
+// state is queried first: a second hipHostRegister of a registered range made the
+// owner's later hipHostUnregister fail.)
 hipError_t register_range(void* ptr, uint64_t bytes, bool& own) {
-  const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
-  if (e == hipErrorHostMemoryAlreadyRegistered) {
-    (void)hipGetLastError();  // (clear the sticky-free error state)
+  unsigned int flags = 0;
+  if (hipHostGetFlags(&flags, ptr) == hipSuccess) {
     own = false;
     return hipSuccess;
   }
+  (void)hipGetLastError();  // (pageable: the query's error is expected)
+  const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
   own = e == hipSuccess;
   return e;
 }
