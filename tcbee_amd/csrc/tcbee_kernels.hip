@@ -1582,11 +1582,21 @@ void k_count_chunk2(CountArgs c) {
   const uint64_t nflows = c.batch->flow_total;
   if (count_mode(c, nflows) != 1 || !chunk_scatter(c, nflows)) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);  // spare bucket: nb
+  const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);
+  // The chunk is sorted by SUB-BIN = claim >> sh, the finest key whose bins fit the
+  // LDS counters (<= kChunkMaxNb - 1 of them): a refinement of the bucket order
+  // (claim >> kBucketBits), so each bucket is still one contiguous run of the chunk,
+  // but neighbouring lanes of the sorted walk gather claim -> id from fewer lines
+  // (125k flows: bins of 256 claims = 1 KiB of omap instead of 16 KiB; 1M flows:
+  // 2048 claims) and the ranking's adds spread over more LDS addresses.
+  uint32_t sh = 8;
+  while (sh < kBucketBits && ((nflows + (1ull << sh) - 1) >> sh) >= kChunkMaxNb) ++sh;
+  const uint32_t nsb = (uint32_t)((nflows + (1ull << sh) - 1) >> sh);  // spare sub-bin: nsb
+  const uint32_t rsh = kBucketBits - sh;  // bucket j starts at sub-bin j << rsh
   const uint64_t n_acc = c.batch->n_acc;
   const uint64_t nchunks = (n_acc + CH - 1) / CH;
   const uint32_t lmax = 0xFFFFFFFFu >> c.pack_bits;
-  for (uint32_t b = tid; b <= nb; b += BS) s_ch[b] = 0;
+  for (uint32_t b = tid; b <= nsb; b += BS) s_ch[b] = 0;
   __syncthreads();
   for (uint64_t q = blockIdx.x; q < nchunks; q += gridDim.x) {
     const uint64_t base = q * CH;
@@ -1637,7 +1647,7 @@ void k_count_chunk2(CountArgs c) {
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const bool valid = (uint32_t)k * BS + tid < nval;
-      const uint32_t bk = w[k] == 0xFFFFFFFFu ? nb : (w[k] & 0x1FFFFFu) >> kBucketBits;
+      const uint32_t bk = w[k] == 0xFFFFFFFFu ? nsb : (w[k] & 0x1FFFFFu) >> sh;
       const uint32_t b0 = __builtin_amdgcn_readfirstlane(bk);
       const uint64_t vm = __ballot(valid);
       if (__all(!valid || bk == b0)) {
@@ -1653,17 +1663,20 @@ void k_count_chunk2(CountArgs c) {
     __syncthreads();
     {
       uint32_t tot;
-      const uint32_t off = block1024_excl_scan<BS>(tid <= nb ? s_ch[tid] : 0u, s_w, tot);
-      if (tid <= nb) s_co[tid] = off;
-      if (tid <= nb) c.coffs[q * (kChunkMaxNb + 1) + tid] = off;  // [nb] = end of the real buckets
-      if (tid <= nb) s_ch[tid] = 0;  // read by the scan only: zero for the next chunk
+      const uint32_t off = block1024_excl_scan<BS>(tid <= nsb ? s_ch[tid] : 0u, s_w, tot);
+      if (tid <= nsb) s_co[tid] = off;
+      if (tid <= nsb) s_ch[tid] = 0;  // read by the scan only: zero for the next chunk
     }
     __syncthreads();
+    // the bucket pass's offsets: bucket j = sub-bins [j << rsh, (j + 1) << rsh); [nb] =
+    // the end of the real buckets (the spare sub-bin's start)
+    for (uint32_t j = tid; j <= nb; j += BS)
+      c.coffs[q * (kChunkMaxNb + 1) + j] = s_co[j < nb ? j << rsh : nsb];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const uint32_t pos = (uint32_t)k * BS + tid;
       if (pos >= nval) continue;
-      const uint32_t bk = w[k] == 0xFFFFFFFFu ? nb : (w[k] & 0x1FFFFFu) >> kBucketBits;
+      const uint32_t bk = w[k] == 0xFFFFFFFFu ? nsb : (w[k] & 0x1FFFFFu) >> sh;
       s_pos[s_co[bk] + lp[k]] = (uint16_t)pos;
       s_rw[pos] = w[k];
     }
@@ -1688,7 +1701,7 @@ void k_count_chunk2(CountArgs c) {
           }
         }
         rg[idx] = (cl & (kBucket - 1u)) | l << kBucketBits;  // coalesced runs
-        id = c.omap[cl];  // one bucket's 16 KiB window per wave
+        id = c.omap[cl];  // a few sub-bins' windows per wave: few lines
       }
       s_rw[pos] = id;  // only this thread reads or writes slot pos in this phase
     }
