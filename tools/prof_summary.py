@@ -1,27 +1,43 @@
 #!/usr/bin/env python3
-"""Turn rocprofv3 outputs under gpurun_out/ into committed summaries under profiles/.
+"""Turn one box's rocprofv3 outputs (tools/r05_prof.sh) into committed summaries.
 
-  python tools/prof_summary.py ROUND_TAG
-reads  gpurun_out/prof/run_kernel_stats.csv (+ run_kernel_trace.csv)
-       gpurun_out/pmc_fetch/run_counter_collection.csv, gpurun_out/pmc_write/...
-writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_summary.md,
-       profiles/pmc_k_parse.json (read by bench.py for roofline.traffic)
+  python tools/prof_summary.py TAG [--prefix r05prof]
 
-HBM traffic per k_parse launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes):
-on gfx950 FETCH_SIZE counts exactly half the bytes of a wide streaming read
-(MI355X_MICROARCH.md "HBM"); calibrated on this kernel by the 64-B workload,
-whose reads are known (arena 64 B + index 20 B per frame).
+reads only the directories of THIS run (no stale gpurun_out/ entries of older rounds):
+  gpurun_out/<prefix>_c3/   kernel trace + stats of the headline command, and
+  gpurun_out/<prefix>_c3.json  the bench line that same process printed
+  gpurun_out/<prefix>_c4v8/ one GPU's flow-hash share of config 4 at N=8 (+ .json)
+  gpurun_out/<prefix>_c4/   the whole 1M-flow config-4 trace on one GPU (+ .json)
+  gpurun_out/pmc_<leg>_{fetch,write,rdreq}/  K1 PMC passes (tools/pmc_c4.sh), legs
+                            c3 / c4v8 / c4 / v6 when present and newer than the trace
+writes profiles/<TAG>_summary.md, <TAG>_kernel_stats.csv, <TAG>_bench.json,
+       <TAG>_config4_share_kernel_stats.csv, <TAG>_config4_whole_kernel_stats.csv,
+       <TAG>_pmc_<leg>_*.csv, <TAG>_pmc_legs.json and profiles/pmc_k_parse.json (read by
+       bench.py for roofline.traffic).
+
+HBM traffic per k_parse launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on
+gfx950 FETCH_SIZE counts half the bytes of a wide streaming read (MI355X_MICROARCH.md
+"HBM"); the doubling is confirmed on this kernel by the TCC_EA0_RDREQ_128B pass.
 """
+import argparse
 import csv
 import json
 import os
+import re
 import shutil
 import statistics
-import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
+
+LEGS = {"c3": ("config 3: 100M IMIX frames, 10k flows", "", "--no-extra --no-cpu"),
+        "c4v8": ("config 4, one GPU's flow-hash share at N=8: ~125M frames, ~125k flows",
+                 "--config4 --virtual-world 8",
+                 "--config4 --virtual-world 8 --steps 5 --warmup 1 --no-cpu --no-extra"),
+        "c4": ("config 4, the whole 1M-flow trace on one GPU: 125M IMIX frames",
+               "--config4", "--config4 --shard contig --steps 5 --warmup 1 --no-cpu --no-extra"),
+        "v6": ("config 3 over IPv6/TCP: 100M IMIX6 frames, 10k flows", "--sizes imix6", "")}
 
 
 def pmc_values(path, kernel_sub):
@@ -29,102 +45,89 @@ def pmc_values(path, kernel_sub):
     return [float(r["Counter_Value"]) for r in rows if kernel_sub in r["Kernel_Name"]]
 
 
-def leg_frames(leg: str) -> int:
-    """Frames per k_parse launch of a PMC leg: the bench's own "<n> frames resident"
-    log line (gpurun_out/pmc_<leg>_fetch.log, tools/pmc_c4.sh), else the nominal config size."""
-    import re
-    log = os.path.join(OUT, f"pmc_{leg}_fetch.log")
+def frames_of(log_path, fallback):
     try:
-        m = re.search(r"rank 0: (\d+) frames resident", open(log).read())
+        m = re.search(r"rank 0: (\d+) frames resident", open(log_path).read())
         if m:
             return int(m.group(1))
     except OSError:
         pass
-    if leg == "c4v8":
-        sys.exit(f"{log}: no 'frames resident' line (the shard size is seed-dependent)")
-    return 100_000_000 if leg == "c3" else 125_000_000
+    return fallback
+
+
+def stats_table(path):
+    rows = ["| kernel | calls | avg us | min us | max us |", "|---|---|---|---|---|"]
+    for r in csv.DictReader(open(path)):
+        if "tcbee" in r["Name"]:
+            rows.append(f"| `{r['Name'].split('(')[0].replace('void ', '')[:60]}` | {r['Calls']} | "
+                        f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['MinNs']) / 1e3:.1f} | "
+                        f"{float(r['MaxNs']) / 1e3:.1f} |")
+    return rows
+
+
+def trace_k1(path):
+    """k_parse launches of a kernel trace: (all-launch average us, timed-step average
+    us = the launches after the warm-up ones, their count)."""
+    ds = [(int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+          for r in csv.DictReader(open(path)) if "k_parse" in r["Kernel_Name"]]
+    ds = [d for _, d in sorted(ds)]
+    return statistics.mean(ds) if ds else None, ds
 
 
 def main():
-    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
-    if tag.startswith("-") or "/" in tag:
-        sys.exit(f"usage: {sys.argv[0]} ROUND_TAG  (a tag such as r03; got {tag!r})")
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--prefix", default="r05prof")
+    a = ap.parse_args()
+    tag, pre = a.tag, a.prefix
     os.makedirs(PROF, exist_ok=True)
     lines = [f"# rocprofv3 summary — {tag}", ""]
-    stats = os.path.join(OUT, "prof", "run_kernel_stats.csv")
-    if os.path.exists(stats):
-        shutil.copy(stats, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
-        lines += ["Command: `rocprofv3 --kernel-trace --stats -- python bench.py --steps 10 "
-                  "--no-cpu --no-extra --sample-check` (config 3: 100M IMIX frames, 10k flows).", "",
-                  "| kernel | calls | avg us | total % |", "|---|---|---|---|"]
-        for r in csv.DictReader(open(stats)):
-            lines.append(f"| `{r['Name'][:70]}` | {r['Calls']} | "
-                         f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} |")
-        lines.append("")
-    f = os.path.join(OUT, "pmc_fetch", "run_counter_collection.csv")
-    w = os.path.join(OUT, "pmc_write", "run_counter_collection.csv")
-    if not os.path.exists(f):  # tools/pmc_c4.sh layout (config-3 leg)
-        f = os.path.join(OUT, "pmc_c3_fetch", "run_counter_collection.csv")
-        w = os.path.join(OUT, "pmc_c3_write", "run_counter_collection.csv")
-    if os.path.exists(f) and os.path.exists(w):
-        fk = pmc_values(f, "k_parse")
-        wk = pmc_values(w, "k_parse")
-        fetch = statistics.median(fk) * 1024 * 2
-        write = statistics.median(wk) * 1024
-        traffic = fetch + write
-        pmc = {"kernel": "k_parse", "workload": "config3 100M IMIX 10k flows",
-               "frames": 100_000_000, "sizes": "imix", "flows": 10_000,
-               "fetch_bytes_corrected": fetch, "write_bytes": write,
-               "traffic_bytes_per_launch": traffic, "fetch_size_kib_raw": statistics.median(fk),
-               "write_size_kib_raw": statistics.median(wk), "dispatches": len(fk),
-               "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE, KiB->B"}
-        json.dump(pmc, open(os.path.join(PROF, "pmc_k_parse.json"), "w"), indent=1)
-        lines += ["## HBM traffic of k_parse (separate --pmc passes)", "",
-                  f"- FETCH_SIZE {statistics.median(fk):.0f} KiB raw -> {fetch / 1e9:.2f} GB "
-                  "(x2 gfx950 correction)",
-                  f"- WRITE_SIZE {statistics.median(wk):.0f} KiB -> {write / 1e9:.2f} GB",
-                  f"- traffic per launch {traffic / 1e9:.2f} GB = {traffic / 1e8:.1f} B/frame "
-                  "(algorithmic 156 B/frame)", ""]
-        for name in ("pmc_fetch", "pmc_write"):
-            src = os.path.join(OUT, name, "run_counter_collection.csv")
-            if not os.path.exists(src):
-                src = os.path.join(OUT, name.replace("pmc_", "pmc_c3_"), "run_counter_collection.csv")
-            dst = os.path.join(PROF, f"{tag}_{name}.csv")
-            with open(src) as fi, open(dst, "w") as fo:
-                rd = csv.DictReader(fi)
-                cols = ["Dispatch_Id", "Kernel_Name", "Grid_Size", "Workgroup_Size",
-                        "LDS_Block_Size", "VGPR_Count", "Counter_Name", "Counter_Value"]
-                wr = csv.writer(fo)
-                wr.writerow(cols)
-                for r in rd:
-                    if "tcbee" in r["Kernel_Name"]:
-                        wr.writerow([r[c] for c in cols])
-    c4 = os.path.join(OUT, "c4prof", "run_kernel_stats.csv")
-    if os.path.exists(c4):
-        shutil.copy(c4, os.path.join(PROF, f"{tag}_config4_kernel_stats.csv"))
-        lines += ["## config 4, one GPU's share", "",
-                  "Command: `rocprofv3 --kernel-trace --stats -- python bench.py --config4 "
-                  "--virtual-world 8 --steps 5 --warmup 1 --no-cpu --no-extra --sample-check` "
-                  "(rank 0's flow-hash shard of 1B IMIX frames / 8 GPUs: ~125M frames, "
-                  "~125k flows).", "",
-                  "| kernel | calls | avg us | total % |", "|---|---|---|---|"]
-        for r in csv.DictReader(open(c4)):
-            if "tcbee" in r["Name"]:
-                lines.append(f"| `{r['Name'][:70]}` | {r['Calls']} | "
-                             f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} |")
-        lines.append("")
-    legs = {"c3": ("config 3: 100M IMIX frames, 10k flows", ""),
-            "c4": ("config 4, whole 1M-flow trace on one GPU: 125M IMIX frames", "--config4"),
-            "c4v8": ("config 4, one GPU's flow-hash share at N=8: ~125M frames, ~125k flows",
-                     "--config4 --virtual-world 8"),
-            "v6": ("config 3 over IPv6/TCP: 100M IMIX6 (78/576/1500) frames, 10k flows",
-                   "--sizes imix6")}
+    c3 = os.path.join(OUT, f"{pre}_c3")
+    if os.path.isdir(c3):
+        shutil.copy(os.path.join(c3, "run_kernel_stats.csv"), os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+        line = next(ln for ln in open(os.path.join(OUT, f"{pre}_c3.json")) if ln.startswith("{"))
+        open(os.path.join(PROF, f"{tag}_bench.json"), "w").write(line)
+        b = json.loads(line)
+        avg, ds = trace_k1(os.path.join(c3, "run_kernel_trace.csv"))
+        timed = ds[b["warmup"]:b["warmup"] + b["steps"]]
+        n = b["config"]["frames_per_gpu"]
+        alg = n * b["roofline"]["alg_bytes_per_frame"]
+        lines += [f"Command: `rocprofv3 --kernel-trace --stats -- python bench.py {LEGS['c3'][2]}` "
+                  f"({LEGS['c3'][0]}); the bench line below is the one this process printed.", ""]
+        lines += stats_table(os.path.join(c3, "run_kernel_stats.csv")) + [""]
+        lines += [f"k_parse: {len(ds)} launches, average {avg:.1f} us over all of them (warm-up "
+                  f"included); the {len(timed)} timed steps' launches average "
+                  f"{statistics.mean(timed):.1f} us -> {alg / statistics.mean(timed) / 1e3:.1f} GB/s "
+                  f"algorithmic = frac {alg / statistics.mean(timed) / 1e3 / 8000:.4f} of 8 TB/s; "
+                  f"the line's HIP-event K1 {b['roofline']['k1_ms'] * 1e3:.1f} us "
+                  f"(frac {b['roofline']['frac']}).", "",
+                  "```", line.strip(), "```", ""]
+    for leg, name, title in (("c4v8", "config4_share", "config 4, one GPU's flow-hash share at N=8"),
+                             ("c4", "config4_whole", "config 4, the whole 1M-flow trace on one GPU")):
+        d = os.path.join(OUT, f"{pre}_{leg}")
+        if not os.path.isdir(d):
+            continue
+        shutil.copy(os.path.join(d, "run_kernel_stats.csv"), os.path.join(PROF, f"{tag}_{name}_kernel_stats.csv"))
+        lines += [f"## {title}", "",
+                  f"Command: `rocprofv3 --kernel-trace --stats -- python bench.py {LEGS[leg][2]}`.", ""]
+        lines += stats_table(os.path.join(d, "run_kernel_stats.csv")) + [""]
+        try:
+            ln = next(x for x in open(os.path.join(OUT, f"{pre}_{leg}.json")) if x.startswith("{"))
+            bl = json.loads(ln)
+            lines += [f"Line: {bl['value']} Mpkt/s, {bl['ms_per_step']} ms/step, K1 "
+                      f"{bl['roofline']['k1_ms']} ms (events), frames {bl['check'].get('frames_local', bl['config'].get('frames_per_gpu'))}, "
+                      f"flows {bl['check'].get('flows')}.", ""]
+        except (OSError, StopIteration):
+            pass
     pmc_legs = {}
-    for leg, (what, args) in legs.items():
+    t_trace = os.path.getmtime(c3) if os.path.isdir(c3) else 0
+    for leg, (what, args, _) in LEGS.items():
         paths = {k: os.path.join(OUT, f"pmc_{leg}_{k}", "run_counter_collection.csv")
                  for k in ("fetch", "write", "rdreq")}
         if not all(os.path.exists(x) for x in paths.values()):
             continue
+        if min(os.path.getmtime(x) for x in paths.values()) < t_trace - 3600:
+            continue  # an older box's passes
         fk = statistics.median(pmc_values(paths["fetch"], "k_parse"))
         wk = statistics.median(pmc_values(paths["write"], "k_parse"))
         rd = {}
@@ -132,9 +135,8 @@ def main():
             if "k_parse" in r["Kernel_Name"]:
                 rd.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
         rd = {k: statistics.median(v) for k, v in rd.items()}
-        # frames the PMC'd k_parse launches parsed: from the leg's bench log ("N frames
-        # resident"), written beside the counter CSVs by tools/pmc_c4.sh
-        frames = leg_frames(leg)
+        frames = frames_of(os.path.join(OUT, f"pmc_{leg}_fetch.log"),
+                           100_000_000 if leg in ("c3", "v6") else 125_000_000)
         fetch, write = fk * 1024 * 2, wk * 1024
         pmc_legs[leg] = {"workload": what, "command": "bench.py --steps 2 --warmup 1 --no-cpu "
                          f"--no-extra --sample-check {args}".strip(), "frames": frames,
@@ -153,6 +155,16 @@ def main():
                 for r in rdr:
                     if "tcbee" in r["Kernel_Name"]:
                         wr.writerow([r[c] for c in cols])
+        if leg == "c3":  # bench.py's roofline.traffic (pmc_traffic reads these keys)
+            json.dump({"kernel": "k_parse", "workload": "config3 100M IMIX 10k flows",
+                       "frames": frames, "sizes": "imix", "flows": 10000,
+                       "fetch_bytes_corrected": fetch, "write_bytes": write,
+                       "traffic_bytes_per_launch": fetch + write, "fetch_size_kib_raw": fk,
+                       "write_size_kib_raw": wk,
+                       "dispatches": len(pmc_values(paths["fetch"], "k_parse")),
+                       "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE, KiB->B",
+                       "source": f"profiles/{tag}_pmc_c3_fetch.csv + {tag}_pmc_c3_write.csv"},
+                      open(os.path.join(PROF, "pmc_k_parse.json"), "w"), indent=1)
     if pmc_legs:
         json.dump(pmc_legs, open(os.path.join(PROF, f"{tag}_pmc_legs.json"), "w"), indent=1)
         lines += ["## k_parse HBM-side traffic per leg (separate --pmc passes; FETCH x2)", "",
@@ -162,40 +174,6 @@ def main():
             lines.append(f"| {v['workload']} | {v['read_B_per_frame']} | {v['write_B_per_frame']} | "
                          f"{v['traffic_B_per_frame']} | {v['rdreq_per_frame']} |")
         lines.append("")
-    c4f = os.path.join(OUT, "c4fprof", "run_kernel_stats.csv")
-    if os.path.exists(c4f):
-        shutil.copy(c4f, os.path.join(PROF, f"{tag}_config4_whole_kernel_stats.csv"))
-        lines += ["## config 4, the whole 1M-flow trace on one GPU", "",
-                  "Command: `rocprofv3 --kernel-trace --stats -- python bench.py --config4 "
-                  "--shard contig --steps 5 --warmup 1 --no-cpu --no-extra --sample-check` "
-                  "(125M IMIX frames, 1M flows: every flow in one table).", "",
-                  "| kernel | calls | avg us | total % |", "|---|---|---|---|"]
-        for r in csv.DictReader(open(c4f)):
-            if "tcbee" in r["Name"]:
-                lines.append(f"| `{r['Name'][:70]}` | {r['Calls']} | "
-                             f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} |")
-        lines.append("")
-    small = os.path.join(OUT, "smallprof", "run_kernel_stats.csv")
-    if os.path.exists(small):
-        shutil.copy(small, os.path.join(PROF, f"{tag}_config2_kernel_stats.csv"))
-        lines += ["## config 2 (1M x 64 B, 1 flow)", "",
-                  "Command: `rocprofv3 --kernel-trace --stats -- python tools/k1_sweep.py "
-                  "--frames 1000000 --fpl 2 --workloads 64B1 --rounds 1 --iters 20` "
-                  "(flows on and off variants).", "",
-                  "| kernel | calls | avg us | total % |", "|---|---|---|---|"]
-        for r in csv.DictReader(open(small)):
-            if "tcbee" in r["Name"]:
-                lines.append(f"| `{r['Name'][:70]}` | {r['Calls']} | "
-                             f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} |")
-        lines.append("")
-    bench_log = os.path.join(OUT, "bench.log")
-    if os.path.exists(bench_log):
-        for ln in open(bench_log):
-            if ln.startswith("{"):
-                shutil.copy(bench_log, os.path.join(PROF, f"{tag}_bench.json"))
-                with open(os.path.join(PROF, f"{tag}_bench.json"), "w") as fo:
-                    fo.write(ln)
-                lines += ["## bench.py line", "", "```", ln.strip(), "```", ""]
     open(os.path.join(PROF, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
