@@ -105,8 +105,10 @@ def rss_for(torch, n_global, world, kind, n_flows, seed, stream):
         if len(table) % world == 0:  # the modulo placement on the same window, for reference
             mod = np.bincount(np.arange(len(table)) % world, weights=load, minlength=world)
             info["rss"]["window_imbalance_modulo"] = round(float(mod.max() / mod.mean()), 5)
+    # (the multi-flow IPv4 kind: each flow's key from its number; any other kind is
+    #  bounded by its flow count on every rank)
     flows_per_rank = (tcbee_amd.rss_flows_per_rank(n_flows, world, seed, table)
-                      if kind == 1 else np.full(world, n_flows if world == 1 else 1, np.int64))
+                      if kind == 1 else np.full(world, n_flows, np.int64))
     skew = float(flows_per_rank.max() / max(flows_per_rank.mean(), 1e-9))
     if world >= 2 and kind == 1:
         info["flows_per_rank"] = [int(flows_per_rank.min()), int(flows_per_rank.max())]
