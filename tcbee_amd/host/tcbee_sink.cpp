@@ -15,7 +15,12 @@
 //   - by default the whole run is one transaction (the reference autocommits
 //     every statement); TCBEE_SINK_DURABLE restores per-statement commits;
 //   - row ids come from sqlite3_last_insert_rowid instead of re-SELECTing the
-//     row just inserted (same value: AUTOINCREMENT ids, UNIQUE keys).
+//     row just inserted (same value: AUTOINCREMENT ids, UNIQUE keys);
+//   - a full batch (1001 points) is ONE prepared multi-row INSERT (the reference's
+//     own statement shape, its parameters bound instead of formatted into the text);
+//     partial batches (the flush at close) go row by row inside a SAVEPOINT (1.9x
+//     fewer seconds per record than row by row everywhere; foreign keys stay
+//     enforced per row — verifying them once at close saved only 9 % more).
 #include "tcbee_host_internal.h"
 
 #include <sqlite3.h>
@@ -155,6 +160,7 @@ struct tcbee_sink {
   sqlite3_stmt* ins_series = nullptr;
   sqlite3_stmt* del_series = nullptr;
   sqlite3_stmt* ins_point[4] = {};
+  sqlite3_stmt* ins_batch[4] = {};  // full batches: kBufferSize + 1 rows, prepared on first use
   std::vector<FlowTracker*> flows;                          // creation order
   std::unordered_map<TupleKey, uint32_t, TupleHash> index;  // DBWriter::streams
   tcbee_sink_stats st{};
@@ -216,6 +222,33 @@ int delete_series(tcbee_sink* s, int64_t flow_id, const char* name) {
 int insert_points(tcbee_sink* s, int64_t series_id, int type, const double* t,
                   const int64_t* iv, const double* fv, const char* const* tv, uint64_t n) {
   if (n == 0) return TCBEE_EDB;  // "INSERT ... VALUES;" is a syntax error
+  if (n == kBufferSize + 1) {
+    // a full TsTracker batch: one multi-row statement (a constraint failure rolls
+    // the whole statement back: all rows or none, as the reference's)
+    sqlite3_stmt*& st = s->ins_batch[type];
+    if (!st) {
+      std::string q = std::string("INSERT INTO time_series_data (time_series_id, timestamp, ") +
+                      value_column(type) + ") VALUES ";
+      for (uint64_t i = 0; i < n; ++i) q += i ? ",(?,?,?)" : "(?,?,?)";
+      if (prep(s->db, q.c_str(), &st)) return TCBEE_EDB;
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+      const int b = int(3 * i);
+      sqlite3_bind_int64(st, b + 1, series_id);
+      sqlite3_bind_double(st, b + 2, t[i]);
+      if (type == kFloat) sqlite3_bind_double(st, b + 3, fv[i]);
+      else if (type == kText) sqlite3_bind_text(st, b + 3, tv[i], -1, SQLITE_STATIC);
+      else sqlite3_bind_int64(st, b + 3, iv[i]);
+    }
+    const int rc = step_done(st);
+    if (rc == TCBEE_OK) {
+      s->st.points += n;
+      ++s->st.batches;
+    } else {
+      ++s->st.failed_batches;
+    }
+    return rc;
+  }
   if (exec(s->db, "SAVEPOINT tcbee_batch")) return TCBEE_EDB;
   sqlite3_stmt* st = s->ins_point[type];
   int rc = TCBEE_OK;
@@ -342,7 +375,8 @@ int fail_marker(tcbee_sink* s) {
 void free_sink(tcbee_sink* s) {
   for (FlowTracker* f : s->flows) delete f;
   sqlite3_stmt* all[] = {s->ins_flow, s->del_flow, s->ins_series, s->del_series,
-                         s->ins_point[0], s->ins_point[1], s->ins_point[2], s->ins_point[3]};
+                         s->ins_point[0], s->ins_point[1], s->ins_point[2], s->ins_point[3],
+                         s->ins_batch[0], s->ins_batch[1], s->ins_batch[2], s->ins_batch[3]};
   for (sqlite3_stmt* st : all)
     if (st) sqlite3_finalize(st);
   if (s->db) sqlite3_close(s->db);

@@ -275,6 +275,10 @@ def test_sink_wedge_and_flags_match_oracle(tmp_path):
     ids = key_ids(records)
     g, gst, err = sink_dump(tmp_path, "g", lambda s: s.packets_grouped(records, ids))
     assert err is None and g == o and gst == ost
+    # (a rejected full batch is one multi-row statement rolled back whole; per-statement
+    #  commits too)
+    d, dst, err = sink_dump(tmp_path, "d", lambda s: s.packets(records), durable=True)
+    assert err is None and d == o and dst == ost
     flagged = [r for r in o["time_series_data"] if r[2] == 1]
     assert flagged, "FLAG_* points land in value_boolean"
 
