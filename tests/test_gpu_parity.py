@@ -562,6 +562,45 @@ def test_k3_range_mode_large_batches(gpu, oracle, pool, n, k3v, monkeypatch):
         assert p.count_mode() == (3 if len(table) <= 3 * 12288 else 1)
 
 
+@pytest.mark.parametrize("flows", [130_560, 130_561, 261_120, 261_121])
+def test_k3_chunk_sub_bin_boundaries(gpu, oracle, flows):
+    """Mode 1's chunk sort bins claims by claim >> sh, sh the smallest shift >= 8
+    that keeps a chunk's bins under 511 (tcbee_kernels.hip k_count_chunk2): 130560
+    flows = 510 bins of 256 (sh 8, every bin used), 130561 the first count at sh 9,
+    261120 / 261121 the same edge of sh 9 -> 10. Every flow appears (16 frames per
+    flow of the per-frame draw; checked: the table has exactly
+    `flows` entries); ids, records and the table vs the oracle."""
+    import torch
+    n = 16 * flows
+    tr = tcbee_amd.synth_trace(n, sizes="64", kind=1, n_flows=flows, seed=flows)
+    d_arena = torch.from_numpy(np.concatenate([tr.arena, np.zeros(64, np.uint8)])).cuda()
+    d_off = torch.from_numpy(tr.offset.view(np.int64)).cuda()
+    d_len = torch.from_numpy(tr.caplen.view(np.int32)).cuda()
+    d_ts = torch.from_numpy(tr.ts_ns.view(np.int64)).cuda()
+    rec_d = torch.empty(n * 74 + 64, dtype=torch.uint8, device="cuda")
+    fi_d = torch.empty(n, dtype=torch.int32, device="cuda")
+    n_d = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctr_d = torch.zeros(4, dtype=torch.int64, device="cuda")
+    with tcbee_amd.PacketParser(max_frames=n, max_flows=flows + flows // 16) as p:
+        s = torch.cuda.current_stream().cuda_stream
+        p.parse_device(d_arena, len(tr.arena), d_off, d_len, d_ts, n, rec_d, n, None, fi_d, n_d,
+                       ctr_d, stream=s)
+        torch.cuda.synchronize()
+        ft = oracle.new_flowtab(1 << 20)
+        try:
+            rec, fh, fi, ctr, _ = oracle.parse(tr, ft=ft)
+            table = oracle.flows(ft)
+        finally:
+            oracle.free_flowtab(ft)
+        assert len(table) == flows
+        k = int(n_d.item())
+        assert k == len(rec) == n
+        assert np.array_equal(fi_d[:k].cpu().numpy().view(np.uint32), fi)
+        assert np.array_equal(rec_d[:k * 74].cpu().numpy().reshape(-1, 74), rec)
+        assert np.array_equal(p.flows(), table)
+        assert p.status() == 0 and p.count_mode() == 1
+
+
 @pytest.mark.parametrize("reset", [False, True])
 @pytest.mark.parametrize("flows", [300, 40_000])
 def test_async_ids_stream_batches(gpu, oracle, reset, flows):
