@@ -31,7 +31,8 @@ def free_port() -> int:
 
 
 def launch(world: int, args: list[str], timeout: int, **env_extra):
-    env = dict(os.environ, TCBEE_DIST_BACKEND="gloo", PYTHONUNBUFFERED="1", **env_extra)
+    env = dict(os.environ, TCBEE_DIST_BACKEND="gloo", PYTHONUNBUFFERED="1")
+    env.update(env_extra)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
            "--master-port", str(free_port()), "bench.py", "--gpus", str(world)] + args
@@ -39,8 +40,8 @@ def launch(world: int, args: list[str], timeout: int, **env_extra):
                           timeout=timeout)
 
 
-def run_bench_world(world: int, args: list[str], timeout: int = 420) -> dict:
-    r = launch(world, args, timeout)
+def run_bench_world(world: int, args: list[str], timeout: int = 420, **env_extra) -> dict:
+    r = launch(world, args, timeout, **env_extra)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints ONE line
@@ -110,3 +111,21 @@ def test_bench_skewed_rss_refused_before_timing(gpu):
     assert "steps in" not in r.stderr  # bench.run_device's "N steps in X ms" never logged
     assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert time.perf_counter() - t0 < 240
+
+
+@pytest.mark.parametrize("shard", ["flowhash", "contig"])
+def test_bench_world1_over_rccl(gpu, shard):
+    """The RCCL branch of the exchange (dist.all_gather_flat / all_to_all_flat on
+    "nccl", device tensors, no host staging) at world 1: torchrun with one rank,
+    TCBEE_BENCH_FORCE_MERGE=1 so the N>1 code path (FlowHashExchange for flow-hash
+    shards, OwnerExchange for contiguous ones, the counter all-reduce) runs over a
+    one-rank RCCL communicator — RCCL refuses two ranks on one GPU, so this is the
+    most of the collective path a one-GPU box can run; every record bit-exact."""
+    out = run_bench_world(1, ["--frames", "4000000", "--steps", "2", "--warmup", "1",
+                              "--no-cpu", "--no-extra", "--shard", shard],
+                          TCBEE_DIST_BACKEND="nccl", TCBEE_BENCH_FORCE_MERGE="1")
+    assert out["dist"] == {"backend": "nccl", "world_size": 1}
+    assert out["config"]["shard"] == shard
+    chk = out["check"]
+    check_leg(chk, 1)
+    assert chk["flows"] == 10_000 and chk["pkts_total"] == 4_000_000
