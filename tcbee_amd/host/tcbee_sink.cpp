@@ -8,19 +8,19 @@
 //   delete_time_series / flow attributes    ts-storage/src/sqlite/db.rs
 //
 // Differences in mechanics, not in the resulting database:
-//   - points are inserted through one prepared single-row statement inside a
-//     SAVEPOINT per batch instead of one formatted multi-row INSERT; a
-//     constraint failure rolls the savepoint back, which is the multi-row
-//     statement's all-or-nothing behaviour;
 //   - by default the whole run is one transaction (the reference autocommits
 //     every statement); TCBEE_SINK_DURABLE restores per-statement commits;
 //   - row ids come from sqlite3_last_insert_rowid instead of re-SELECTing the
 //     row just inserted (same value: AUTOINCREMENT ids, UNIQUE keys);
 //   - a full batch (1001 points) is ONE prepared multi-row INSERT (the reference's
 //     own statement shape, its parameters bound instead of formatted into the text);
-//     partial batches (the flush at close) go row by row inside a SAVEPOINT (1.9x
+//     partial batches (the flush at close) go through one prepared single-row
+//     statement inside a SAVEPOINT, rolled back on a constraint failure — the
+//     multi-row statement's all-or-nothing behaviour (the multi-row form: 1.9x
 //     fewer seconds per record than row by row everywhere; foreign keys stay
-//     enforced per row — verifying them once at close saved only 9 % more).
+//     enforced per row — verifying them once at close saved only 9 % more). A
+//     SQLite built with fewer than 3003 host parameters per statement cannot
+//     prepare it; full batches then take the SAVEPOINT path too.
 #include "tcbee_host_internal.h"
 
 #include <sqlite3.h>
@@ -161,6 +161,7 @@ struct tcbee_sink {
   sqlite3_stmt* del_series = nullptr;
   sqlite3_stmt* ins_point[4] = {};
   sqlite3_stmt* ins_batch[4] = {};  // full batches: kBufferSize + 1 rows, prepared on first use
+  bool batch_unprepared[4] = {};    // that prepare failed: full batches row by row
   std::vector<FlowTracker*> flows;                          // creation order
   std::unordered_map<TupleKey, uint32_t, TupleHash> index;  // DBWriter::streams
   tcbee_sink_stats st{};
@@ -222,16 +223,19 @@ int delete_series(tcbee_sink* s, int64_t flow_id, const char* name) {
 int insert_points(tcbee_sink* s, int64_t series_id, int type, const double* t,
                   const int64_t* iv, const double* fv, const char* const* tv, uint64_t n) {
   if (n == 0) return TCBEE_EDB;  // "INSERT ... VALUES;" is a syntax error
-  if (n == kBufferSize + 1) {
+  sqlite3_stmt*& st = s->ins_batch[type];
+  if (n == kBufferSize + 1 && !st && !s->batch_unprepared[type]) {
+    std::string q = std::string("INSERT INTO time_series_data (time_series_id, timestamp, ") +
+                    value_column(type) + ") VALUES ";
+    for (uint64_t i = 0; i < n; ++i) q += i ? ",(?,?,?)" : "(?,?,?)";
+    if (prep(s->db, q.c_str(), &st)) {
+      st = nullptr;  // e.g. SQLITE_MAX_VARIABLE_NUMBER < 3003: row by row below
+      s->batch_unprepared[type] = true;
+    }
+  }
+  if (n == kBufferSize + 1 && st) {
     // a full TsTracker batch: one multi-row statement (a constraint failure rolls
     // the whole statement back: all rows or none, as the reference's)
-    sqlite3_stmt*& st = s->ins_batch[type];
-    if (!st) {
-      std::string q = std::string("INSERT INTO time_series_data (time_series_id, timestamp, ") +
-                      value_column(type) + ") VALUES ";
-      for (uint64_t i = 0; i < n; ++i) q += i ? ",(?,?,?)" : "(?,?,?)";
-      if (prep(s->db, q.c_str(), &st)) return TCBEE_EDB;
-    }
     for (uint64_t i = 0; i < n; ++i) {
       const int b = int(3 * i);
       sqlite3_bind_int64(st, b + 1, series_id);
@@ -250,15 +254,15 @@ int insert_points(tcbee_sink* s, int64_t series_id, int type, const double* t,
     return rc;
   }
   if (exec(s->db, "SAVEPOINT tcbee_batch")) return TCBEE_EDB;
-  sqlite3_stmt* st = s->ins_point[type];
+  sqlite3_stmt* row = s->ins_point[type];
   int rc = TCBEE_OK;
   for (uint64_t i = 0; i < n && rc == TCBEE_OK; ++i) {
-    sqlite3_bind_int64(st, 1, series_id);
-    sqlite3_bind_double(st, 2, t[i]);
-    if (type == kFloat) sqlite3_bind_double(st, 3, fv[i]);
-    else if (type == kText) sqlite3_bind_text(st, 3, tv[i], -1, SQLITE_STATIC);
-    else sqlite3_bind_int64(st, 3, iv[i]);
-    rc = step_done(st);
+    sqlite3_bind_int64(row, 1, series_id);
+    sqlite3_bind_double(row, 2, t[i]);
+    if (type == kFloat) sqlite3_bind_double(row, 3, fv[i]);
+    else if (type == kText) sqlite3_bind_text(row, 3, tv[i], -1, SQLITE_STATIC);
+    else sqlite3_bind_int64(row, 3, iv[i]);
+    rc = step_done(row);
   }
   if (rc != TCBEE_OK) exec(s->db, "ROLLBACK TO tcbee_batch");
   exec(s->db, "RELEASE tcbee_batch");
