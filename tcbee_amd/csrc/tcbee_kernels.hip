@@ -24,7 +24,19 @@
 
 namespace tcbee {
 
-constexpr uint32_t kRecountSpins = 4096;  // ~0.1 ms of polling before recounting
+// Look-back polling bounds, in wall-clock ticks (wall_clock64: 100 MHz on MI355X,
+// hipDeviceAttributeWallClockRate): a wave polls an unpublished predecessor for
+// 10 us before recounting it from the input, then 1 us for each further one.
+// Bounded by time, not by a poll count: a poll is an agent-scope load of a few
+// hundred ns to a few us, and 4096 of them (round 1-4) let a wave spin for
+// milliseconds when a predecessor's XCD had fallen behind -- with a second process's
+// kernels on the GPU, K1 took 20-200x its time alone.
+#ifndef TCBEE_RECOUNT_TICKS
+#define TCBEE_RECOUNT_TICKS 1000
+#endif
+#ifndef TCBEE_RECOUNT_LATE
+#define TCBEE_RECOUNT_LATE 100
+#endif
 // K1's wave priority while a tile's index and header loads are issued (then 0):
 // a starting wave issues its loads ahead of resident waves' parse / record work
 // (config 3 K1 -2.6 %, round 3; priority 3 and a K3 load-phase priority measured
@@ -251,7 +263,7 @@ __device__ uint32_t tile_accept_count(const ParseArgs& a, uint64_t tile);
 
 // Resolves this tile's exclusive prefix (one wave) and publishes its inclusive
 // prefix. Tiles are blockIdx.x: no dispatch order is assumed. A predecessor
-// whose word stays unpublished for kRecountSpins polls (not yet dispatched, or
+// whose word stays unpublished for TCBEE_RECOUNT_TICKS (not yet dispatched, or
 // slow) has its aggregate recounted from the input by this wave, so the walk
 // always terminates; results never depend on which block publishes first.
 template <int TILE>
@@ -262,10 +274,11 @@ __device__ uint64_t lookback_resolve(const ParseArgs& a, uint64_t tile, uint64_t
   uint64_t* status = a.tile_status;
   uint64_t excl = 0;
   int64_t base = (int64_t)tile - 1;
+  int64_t wait = TCBEE_RECOUNT_TICKS;
   for (;;) {
     const int64_t idx = base - (int64_t)lane;
     uint64_t v = idx >= 0 ? ld_agent(status + idx) : kFlagInc;
-    uint32_t spins = 0;
+    int64_t t0 = wall_clock64();
     for (;;) {
       const uint64_t inv = __ballot((v >> 62) == 0);
       if (!inv) break;
@@ -273,11 +286,12 @@ __device__ uint64_t lookback_resolve(const ParseArgs& a, uint64_t tile, uint64_t
       const uint64_t inc = __ballot((v >> 62) == 2);
       const uint64_t need = inc ? (inv & ((inc & (~inc + 1)) - 1)) : inv;
       if (!need) break;
-      if (++spins > kRecountSpins) {
+      if (wall_clock64() - t0 > wait) {
         const uint32_t j = (uint32_t)__ffsll((unsigned long long)need) - 1;
         const uint32_t cnt = tile_accept_count<TILE>(a, (uint64_t)(base - (int64_t)j));
         if (lane == j) v = kFlagAgg | cnt;
-        spins = 0;
+        t0 = wall_clock64();
+        wait = TCBEE_RECOUNT_LATE;
         continue;
       }
       __builtin_amdgcn_s_sleep(1);

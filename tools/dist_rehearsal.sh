@@ -19,6 +19,7 @@ run() {  # name timeout nproc args...
 for s in "$@"; do
   case $s in
     n2)   run dist_n2 600 2 --steps 5 --warmup 2 --c4-frames 40000000 ;;
+    n2full) run dist_n2full 900 2 ;;  # the driver's own N=2 command, default sizes
     n4)   run dist_n4 600 4 --frames 20000000 --steps 5 --warmup 2 --c4-frames 16000000 ;;
     n8)   run dist_n8 600 8 --frames 8000000 --steps 5 --warmup 2 --c4-frames 6000000 ;;
     n2c4) run dist_n2c4 600 2 --config4 --frames 40000000 --steps 3 --warmup 1 ;;
