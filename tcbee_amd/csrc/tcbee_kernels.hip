@@ -30,7 +30,9 @@ namespace tcbee {
 // Bounded by time, not by a poll count: a poll is an agent-scope load of a few
 // hundred ns to a few us, and 4096 of them (round 1-4) let a wave spin for
 // milliseconds when a predecessor's XCD had fallen behind -- with a second process's
-// kernels on the GPU, K1 took 20-200x its time alone.
+// kernels on the GPU, K1 took 20-200x its time alone. A
+// recounted aggregate is also published in the predecessor's status word (a CAS
+// from "unpublished": the value is the one the predecessor itself will store).
 #ifndef TCBEE_RECOUNT_TICKS
 #define TCBEE_RECOUNT_TICKS 1000
 #endif
@@ -264,8 +266,9 @@ __device__ uint32_t tile_accept_count(const ParseArgs& a, uint64_t tile);
 // Resolves this tile's exclusive prefix (one wave) and publishes its inclusive
 // prefix. Tiles are blockIdx.x: no dispatch order is assumed. A predecessor
 // whose word stays unpublished for TCBEE_RECOUNT_TICKS (not yet dispatched, or
-// slow) has its aggregate recounted from the input by this wave, so the walk
-// always terminates; results never depend on which block publishes first.
+// slow) has its aggregate recounted from the input by this wave (and published for
+// it), so the walk always terminates; results never depend on which block
+// publishes first.
 template <int TILE>
 __device__ uint64_t lookback_resolve(const ParseArgs& a, uint64_t tile, uint64_t count,
                                     bool withhold) {
@@ -289,7 +292,13 @@ __device__ uint64_t lookback_resolve(const ParseArgs& a, uint64_t tile, uint64_t
       if (wall_clock64() - t0 > wait) {
         const uint32_t j = (uint32_t)__ffsll((unsigned long long)need) - 1;
         const uint32_t cnt = tile_accept_count<TILE>(a, (uint64_t)(base - (int64_t)j));
-        if (lane == j) v = kFlagAgg | cnt;
+        if (lane == j) {
+          // published on the predecessor's behalf (if it still has not): the other
+          // successors waiting on it stop polling instead of each recounting it
+          v = kFlagAgg | cnt;
+          atomicCAS(reinterpret_cast<unsigned long long*>(status + idx), 0ull,
+                    (unsigned long long)v);
+        }
         t0 = wall_clock64();
         wait = TCBEE_RECOUNT_LATE;
         continue;
