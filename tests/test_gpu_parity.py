@@ -601,6 +601,47 @@ def test_k3_chunk_sub_bin_boundaries(gpu, oracle, flows):
         assert p.status() == 0 and p.count_mode() == 1
 
 
+@pytest.mark.parametrize("flows", [60_000, 250_000])
+def test_ipv6_many_flows(gpu, oracle, flows):
+    """IPv6/TCP IMIX (kind 3) with many flows: every key lives in the wide slots
+    (64-B tag/key slots, not the compact IPv4 ones), K3 in mode 1 (60k flows: 15
+    buckets; 250k: 62, chunk sub-bins of 512 claims); every flow appears (16 frames
+    per flow); records, hashes, ids and the whole table vs the oracle."""
+    import torch
+    n = 16 * flows
+    tr = tcbee_amd.synth_trace(n, sizes="imix6", kind=3, n_flows=flows, seed=flows + 6)
+    d_arena = torch.from_numpy(np.concatenate([tr.arena, np.zeros(64, np.uint8)])).cuda()
+    d_off = torch.from_numpy(tr.offset.view(np.int64)).cuda()
+    d_len = torch.from_numpy(tr.caplen.view(np.int32)).cuda()
+    d_ts = torch.from_numpy(tr.ts_ns.view(np.int64)).cuda()
+    rec_d = torch.empty(n * 74 + 64, dtype=torch.uint8, device="cuda")
+    fh_d = torch.empty(n, dtype=torch.int32, device="cuda")
+    fi_d = torch.empty(n, dtype=torch.int32, device="cuda")
+    n_d = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctr_d = torch.zeros(4, dtype=torch.int64, device="cuda")
+    with tcbee_amd.PacketParser(max_frames=n, max_flows=flows + flows // 16) as p:
+        s = torch.cuda.current_stream().cuda_stream
+        p.parse_device(d_arena, len(tr.arena), d_off, d_len, d_ts, n, rec_d, n, fh_d, fi_d, n_d,
+                       ctr_d, stream=s)
+        torch.cuda.synchronize()
+        ft = oracle.new_flowtab(1 << 20)
+        try:
+            rec, fh, fi, ctr, _ = oracle.parse(tr, ft=ft)
+            table = oracle.flows(ft)
+        finally:
+            oracle.free_flowtab(ft)
+        assert len(table) == flows
+        k = int(n_d.item())
+        assert k == len(rec) == n
+        assert np.array_equal(rec_d[:k * 74].cpu().numpy().reshape(-1, 74), rec)
+        assert np.array_equal(fh_d.cpu().numpy().view(np.uint32), fh)
+        assert np.array_equal(fi_d.cpu().numpy().view(np.uint32), fi)
+        assert np.array_equal(p.flows(), table)
+        assert ctr_d.cpu().numpy().tolist() == [ctr["ingress"], ctr["egress"], ctr["handled"],
+                                                 ctr["dropped"]]
+        assert p.status() == 0 and p.count_mode() == 1
+
+
 @pytest.mark.parametrize("reset", [False, True])
 @pytest.mark.parametrize("flows", [300, 40_000])
 def test_async_ids_stream_batches(gpu, oracle, reset, flows):
