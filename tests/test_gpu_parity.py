@@ -601,6 +601,43 @@ def test_k3_chunk_sub_bin_boundaries(gpu, oracle, flows):
         assert p.status() == 0 and p.count_mode() == 1
 
 
+@pytest.mark.parametrize("flows", [200_000, 1_000_000])
+def test_zipf_many_flows(gpu, oracle, flows):
+    """Zipf(1.1) over many flows: a head flow holding ~12 % of the records beside a
+    long tail, through K3 mode 1 — a chunk's hot sub-bin takes hundreds of records
+    (the ranking's one-add-per-wave path) while most sub-bins hold one or two; ids,
+    records and the table (only the flows that appeared) vs the oracle."""
+    import torch
+    n = 4_000_000
+    tr = tcbee_amd.synth_trace(n, sizes="imix", kind=2, n_flows=flows, seed=flows + 2)
+    d_arena = torch.from_numpy(np.concatenate([tr.arena, np.zeros(64, np.uint8)])).cuda()
+    d_off = torch.from_numpy(tr.offset.view(np.int64)).cuda()
+    d_len = torch.from_numpy(tr.caplen.view(np.int32)).cuda()
+    d_ts = torch.from_numpy(tr.ts_ns.view(np.int64)).cuda()
+    rec_d = torch.empty(n * 74 + 64, dtype=torch.uint8, device="cuda")
+    fi_d = torch.empty(n, dtype=torch.int32, device="cuda")
+    n_d = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctr_d = torch.zeros(4, dtype=torch.int64, device="cuda")
+    with tcbee_amd.PacketParser(max_frames=n, max_flows=flows + flows // 16) as p:
+        s = torch.cuda.current_stream().cuda_stream
+        p.parse_device(d_arena, len(tr.arena), d_off, d_len, d_ts, n, rec_d, n, None, fi_d, n_d,
+                       ctr_d, stream=s)
+        torch.cuda.synchronize()
+        ft = oracle.new_flowtab(1 << 21)
+        try:
+            rec, fh, fi, ctr, _ = oracle.parse(tr, ft=ft)
+            table = oracle.flows(ft)
+        finally:
+            oracle.free_flowtab(ft)
+        k = int(n_d.item())
+        assert k == len(rec) == n and len(table) > 12_288
+        assert int(table["pkts"].max()) > n // 20  # the head flow
+        assert np.array_equal(fi_d[:k].cpu().numpy().view(np.uint32), fi)
+        assert np.array_equal(rec_d[:k * 74].cpu().numpy().reshape(-1, 74), rec)
+        assert np.array_equal(p.flows(), table)
+        assert p.status() == 0 and p.count_mode() == (3 if len(table) <= 3 * 12288 else 1)
+
+
 @pytest.mark.parametrize("flows", [60_000, 250_000])
 def test_ipv6_many_flows(gpu, oracle, flows):
     """IPv6/TCP IMIX (kind 3) with many flows: every key lives in the wide slots
