@@ -487,6 +487,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   const bool withhold = a.withhold_every && (tile % a.withhold_every) == a.withhold_every - 1;
   if (!withhold && tid == 0) lookback_publish(a.tile_status, tile, total);
 
+  bool staged_early = FLOWS;
   if (FLOWS) {
     // phase B: hash, then issue the first probe's loads of every frame: an IPv4-form
     // key's 16-B compact slot + its fs32 (one line), any other key's 64-B wide slot
@@ -533,6 +534,20 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
             Q[f][j] = __builtin_amdgcn_raw_buffer_load_b128(wd_rs, S0[f] * 64u + 16u * j, 0, 0);
         }
       }
+    }
+    // the records' LDS staging while the first probes are in flight, in waves whose
+    // probes are all compact (IPv4-form) ones; a wave with a wide-slot probe (4 x 16-B
+    // loads per frame in flight) stages after the walk, as before (round 5, A/B of 3
+    // alternating rounds, K1: config 3 -2.2 %, the N=8 share -1.1 %, 1M flows -0.8 %,
+    // IPv6 equal; staging early in every wave: config 3 -1.0 %, IPv6 +0.5 %)
+    bool wide_wave = false;
+#pragma unroll
+    for (int f = 0; f < FPL; ++f) wide_wave = wide_wave || (want[f] && !v4k[f]);
+    staged_early = !__any(wide_wave);
+    if (staged_early) {
+#pragma unroll
+      for (int f = 0; f < FPL; ++f)
+        if (acc[f]) lds_put_record(s_rec, rank[f] * kRecBytes, R[f]);
     }
     // phase C: resolve; a miss (new flow, busy slot, a stale snapshot) takes the full
     // upsert. Walk on with plain loads while the slots hold OTHER flows (published,
@@ -621,9 +636,11 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
       }
     }
   }
+  if (!FLOWS || !staged_early) {
 #pragma unroll
-  for (int f = 0; f < FPL; ++f)
-    if (acc[f]) lds_put_record(s_rec, rank[f] * kRecBytes, R[f]);
+    for (int f = 0; f < FPL; ++f)
+      if (acc[f]) lds_put_record(s_rec, rank[f] * kRecBytes, R[f]);
+  }
 
   // (wave 0 resolving the look-back before its own probes instead — its inclusive
   //  prefix published a probe phase earlier — was 22 % slower, round 3)
