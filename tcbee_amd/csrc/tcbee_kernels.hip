@@ -33,12 +33,6 @@ namespace tcbee {
 // kernels on the GPU, K1 took 20-200x its time alone. A
 // recounted aggregate is also published in the predecessor's status word (a CAS
 // from "unpublished": the value is the one the predecessor itself will store).
-#ifndef TCBEE_K1_STAGE_ALL
-#define TCBEE_K1_STAGE_ALL 0
-#endif
-#ifndef TCBEE_K1_LB_EARLY
-#define TCBEE_K1_LB_EARLY 0  // A/B: > 0: wave 0 tries the look-back for this many ticks under the probes
-#endif
 #ifndef TCBEE_RECOUNT_TICKS
 #define TCBEE_RECOUNT_TICKS 1000
 #endif
@@ -325,45 +319,6 @@ __device__ uint64_t lookback_resolve(const ParseArgs& a, uint64_t tile, uint64_t
   return excl;
 }
 
-#if TCBEE_K1_LB_EARLY
-// lookback_resolve's walk without the recount: polls for at most `ticks` in all and
-// gives up (returns false, nothing published) when a predecessor is still missing.
-__device__ bool lookback_try(const ParseArgs& a, uint64_t tile, uint64_t count, bool withhold,
-                             int64_t ticks, uint64_t& excl_out) {
-  const uint32_t lane = __lane_id();
-  if (tile == 0) { excl_out = 0; return true; }
-  uint64_t* status = a.tile_status;
-  uint64_t excl = 0;
-  int64_t base = (int64_t)tile - 1;
-  const int64_t t0 = wall_clock64();
-  for (;;) {
-    const int64_t idx = base - (int64_t)lane;
-    uint64_t v = idx >= 0 ? ld_agent(status + idx) : kFlagInc;
-    for (;;) {
-      const uint64_t inv = __ballot((v >> 62) == 0);
-      if (!inv) break;
-      const uint64_t inc = __ballot((v >> 62) == 2);
-      const uint64_t need = inc ? (inv & ((inc & (~inc + 1)) - 1)) : inv;
-      if (!need) break;
-      if (wall_clock64() - t0 > ticks) return false;
-      __builtin_amdgcn_s_sleep(1);
-      if ((v >> 62) == 0) v = ld_agent(status + idx);
-    }
-    const uint64_t inc = __ballot((v >> 62) == 2);
-    if (inc) {
-      const uint32_t first = (uint32_t)__ffsll((unsigned long long)inc) - 1;
-      excl += wave_sum64(lane <= first ? (v & kValMask) : 0ull);
-      break;
-    }
-    excl += wave_sum64(v & kValMask);
-    base -= 64;
-  }
-  if (lane == 0 && !withhold) st_agent(status + tile, kFlagInc | (excl + count));
-  excl_out = excl;
-  return true;
-}
-#endif
-
 // record -> LDS at byte offset `bo` (even)
 __device__ __forceinline__ void lds_put_record(uint32_t* srec, uint32_t bo, const uint32_t (&R)[19]) {
   uint16_t* s16 = reinterpret_cast<uint16_t*>(srec);
@@ -533,7 +488,6 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   if (!withhold && tid == 0) lookback_publish(a.tile_status, tile, total);
 
   bool staged_early = FLOWS;
-  bool lb_done = false;  // wave 0: the look-back resolved in the probe shadow
   if (FLOWS) {
     // phase B: hash, then issue the first probe's loads of every frame: an IPv4-form
     // key's 16-B compact slot + its fs32 (one line), any other key's 64-B wide slot
@@ -589,22 +543,12 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
     bool wide_wave = false;
 #pragma unroll
     for (int f = 0; f < FPL; ++f) wide_wave = wide_wave || (want[f] && !v4k[f]);
-    staged_early = TCBEE_K1_STAGE_ALL || !__any(wide_wave);
+    staged_early = !__any(wide_wave);
     if (staged_early) {
 #pragma unroll
       for (int f = 0; f < FPL; ++f)
         if (acc[f]) lds_put_record(s_rec, rank[f] * kRecBytes, R[f]);
     }
-#if TCBEE_K1_LB_EARLY
-    // wave 0 tries the look-back while its first probes are in flight (no recount
-    // here: a predecessor still missing after a short poll leaves it to the full
-    // resolve after the walk)
-    if (wave == 0) {
-      uint64_t ex;
-      lb_done = lookback_try(a, tile, total, withhold, TCBEE_K1_LB_EARLY, ex);
-      if (lb_done && lane == 0) s_excl = ex;
-    }
-#endif
     // phase C: resolve; a miss (new flow, busy slot, a stale snapshot) takes the full
     // upsert. Walk on with plain loads while the slots hold OTHER flows (published,
     // another key): within a batch a slot only goes EMPTY -> BUSY -> published, so a
@@ -700,7 +644,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
 
   // (wave 0 resolving the look-back before its own probes instead — its inclusive
   //  prefix published a probe phase earlier — was 22 % slower, round 3)
-  if (wave == 0 && !lb_done) {
+  if (wave == 0) {
     const uint64_t excl = lookback_resolve<TILE>(a, tile, total, withhold);
     if (lane == 0) s_excl = excl;
   }
