@@ -26,7 +26,11 @@
  *   - One tcbee_ctx per host thread / HIP stream. Calls on different contexts
  *     are independent.
  *   - "_device" entry points take DEVICE pointers and a hipStream_t (as void*,
- *     NULL = the context's own stream) and are asynchronous unless stated.
+ *     NULL = the context's own stream, which then first waits for the work
+ *     already queued on HIP's legacy default stream — e.g. a framework's default-
+ *     stream copies of the inputs or zero-fills of the outputs) and are
+ *     asynchronous unless stated. tcbee_ctx_create returns with the context's
+ *     initialisation complete.
  *     Host-pointer entry points copy H2D / D2H through the context's buffers.
  */
 #ifndef TCBEE_AMD_H

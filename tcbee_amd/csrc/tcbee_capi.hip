@@ -57,6 +57,7 @@ struct tcbee_ctx {
   uint32_t* d_len_scratch_s[2] = {nullptr, nullptr};
   int slot = 0, nslot = 1;
   hipEvent_t ev_k2 = nullptr, ev_k3 = nullptr, ev_fin = nullptr;
+  hipEvent_t ev_null = nullptr;  // a NULL-stream call: the legacy default stream's work so far
   bool k3_async = false;        // a K3 is (or may be) running on another stream
   hipStream_t pend_ids = nullptr;  // deferred + async: the ids stream
   uint64_t* d_tile_status = nullptr;
@@ -108,6 +109,21 @@ struct tcbee_ctx {
   std::vector<hipEvent_t> ev;  // pairs
   uint64_t ev_used = 0;
 };
+
+// A call's stream: the caller's, or (NULL) the context's own non-blocking stream,
+// ordered after whatever is already queued on the legacy default stream (a caller's
+// default-stream producers of the inputs, or zero-fills of the outputs, would
+// otherwise race the parse: the context's stream does not wait for that stream).
+static hipError_t ctx_stream(tcbee_ctx* c, void* stream, hipStream_t& s) {
+  if (stream) {
+    s = (hipStream_t)stream;
+    return hipSuccess;
+  }
+  s = c->stream;
+  hipError_t e = hipEventRecord(c->ev_null, nullptr);
+  if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_null, 0);
+  return e;
+}
 static constexpr uint64_t kMaxProfiled = 4096;
 
 namespace {
@@ -224,7 +240,7 @@ int tcbee_ctx_destroy(tcbee_ctx* c) {
       dfree(c->d_len_scratch_s[i]);
     }
   }
-  for (hipEvent_t e : {c->ev_k2, c->ev_k3, c->ev_fin})
+  for (hipEvent_t e : {c->ev_k2, c->ev_k3, c->ev_fin, c->ev_null})
     if (e) (void)hipEventDestroy(e);
   dfree(c->d_tile_status);
   dfree(c->d_new_list);
@@ -339,26 +355,26 @@ int tcbee_ctx_create_ex(tcbee_ctx** out, int device, uint64_t max_frames, uint64
   if ((e = dalloc(&c->tab.wide, 8 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
   // all ones, then every tag word zero (k_table_init sweeps the wide slots only once
   // used): fs words ~0 as a reset leaves them
-  if ((e = hipMemset(c->tab.wide, 0xFF, 64 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
-  if ((e = hipMemset2D(c->tab.wide, 64, 0, 8, c->tab.wide_mask + 1)) != hipSuccess) return fail(map_err(e));
+  if ((e = hipMemsetAsync(c->tab.wide, 0xFF, 64 * (c->tab.wide_mask + 1), c->stream)) != hipSuccess) return fail(map_err(e));
+  if ((e = hipMemset2DAsync(c->tab.wide, 64, 0, 8, c->tab.wide_mask + 1, c->stream)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.wide_used, 1)) != hipSuccess) return fail(map_err(e));
-  if ((e = hipMemset(c->tab.wide_used, 0, 4)) != hipSuccess) return fail(map_err(e));
+  if ((e = hipMemsetAsync(c->tab.wide_used, 0, 4, c->stream)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.cnt, 2 * c->max_flows)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.cmap, c->max_flows)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_persist, 1)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_batch_slot[0], 1)) != hipSuccess) return fail(map_err(e));
   c->d_batch = c->d_batch_slot[0];
-  for (hipEvent_t* ev : {&c->ev_k2, &c->ev_k3, &c->ev_fin})
+  for (hipEvent_t* ev : {&c->ev_k2, &c->ev_k3, &c->ev_fin, &c->ev_null})
     if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
       return fail(map_err(e));
   if ((e = dalloc(&c->d_tile_status, c->max_tiles)) != hipSuccess) return fail(map_err(e));
   // all zero between batches of small contexts (their K3 re-zeroes the words a batch used)
-  if ((e = hipMemset(c->d_tile_status, 0, c->max_tiles * sizeof(uint64_t))) != hipSuccess)
+  if ((e = hipMemsetAsync(c->d_tile_status, 0, c->max_tiles * sizeof(uint64_t), c->stream)) != hipSuccess)
     return fail(map_err(e));
   if ((e = dalloc(&c->d_new_list, c->max_flows)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_bitmap, c->max_words)) != hipSuccess) return fail(map_err(e));
   // all zero between batches from here on (K3 clears the words a batch set)
-  if ((e = hipMemset(c->d_bitmap, 0, c->max_words * sizeof(uint32_t))) != hipSuccess)
+  if ((e = hipMemsetAsync(c->d_bitmap, 0, c->max_words * sizeof(uint32_t), c->stream)) != hipSuccess)
     return fail(map_err(e));
   if ((e = dalloc(&c->d_wprefix, c->max_words)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_bprefix, c->max_sblocks)) != hipSuccess) return fail(map_err(e));
@@ -419,13 +435,13 @@ int tcbee_ctx_create_ex(tcbee_ctx** out, int device, uint64_t max_frames, uint64
     c->tab_alt.cnt = nullptr;
     if ((e = dalloc(&c->tab_alt.slots, 8 * c->nlines)) != hipSuccess) return fail(map_err(e));
     if ((e = dalloc(&c->tab_alt.wide, 8 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
-    if ((e = hipMemset(c->tab_alt.wide, 0xFF, 64 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
-    if ((e = hipMemset2D(c->tab_alt.wide, 64, 0, 8, c->tab.wide_mask + 1)) != hipSuccess) return fail(map_err(e));
+    if ((e = hipMemsetAsync(c->tab_alt.wide, 0xFF, 64 * (c->tab.wide_mask + 1), c->stream)) != hipSuccess) return fail(map_err(e));
+    if ((e = hipMemset2DAsync(c->tab_alt.wide, 64, 0, 8, c->tab.wide_mask + 1, c->stream)) != hipSuccess) return fail(map_err(e));
     if ((e = dalloc(&c->tab_alt.wide_used, 1)) != hipSuccess) return fail(map_err(e));
-    if ((e = hipMemset(c->tab_alt.wide_used, 0, 4)) != hipSuccess) return fail(map_err(e));
+    if ((e = hipMemsetAsync(c->tab_alt.wide_used, 0, 4, c->stream)) != hipSuccess) return fail(map_err(e));
     if ((e = dalloc(&c->tab_alt.cnt, 2 * c->max_flows)) != hipSuccess) return fail(map_err(e));
     if ((e = dalloc(&c->d_persist_alt, 1)) != hipSuccess) return fail(map_err(e));
-    if ((e = hipMemset(c->d_persist_alt, 0, sizeof(PersistState))) != hipSuccess) return fail(map_err(e));
+    if ((e = hipMemsetAsync(c->d_persist_alt, 0, sizeof(PersistState), c->stream)) != hipSuccess) return fail(map_err(e));
     if ((e = launch_table_init(c->tab_alt, c->stream)) != hipSuccess) return fail(map_err(e));
     if ((e = dalloc(&c->d_batch_slot[1], 1)) != hipSuccess) return fail(map_err(e));
     if ((e = dalloc(&c->d_slot_scratch_s[1], c->max_frames)) != hipSuccess) return fail(map_err(e));
@@ -507,7 +523,8 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
   if ((in->arena && !aligned16(in->arena)) || (out_rec74 && !aligned16(out_rec74)))
     return TCBEE_EINVAL;
   const bool flows = (cfg->flags & TCBEE_F_NO_FLOWS) == 0;
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s;
+  TRY_HIP(ctx_stream(c, stream, s));
   TRY_HIP(hipSetDevice(c->device));
   if (async && c->nslot < 2) {
     // first async batch: the second slot (setup, synchronous allocation)
@@ -713,7 +730,8 @@ int tcbee_parse_finish_device(tcbee_ctx* c, const uint32_t* id_map_dev, uint64_t
     return TCBEE_OK;
   }
   TRY_HIP(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s;
+  TRY_HIP(ctx_stream(c, stream, s));
   CountArgs k = c->pend;
   if (id_map_dev && !c->d_omap) TRY_HIP(dalloc(&c->d_omap, c->max_flows));
   hipStream_t ks = s;
@@ -740,7 +758,8 @@ int tcbee_flow_first_frames_device(tcbee_ctx* c, uint64_t* out_first_frame_dev, 
                                    uint64_t rec_frame_cap, void* stream) {
   if (!c || (cap && !out_first_frame_dev) || (n_frames && !frame_gidx_dev)) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s;
+  TRY_HIP(ctx_stream(c, stream, s));
   if (int rc = apply_pending_reset(c, s)) return rc;
   GlobalExportArgs g{};
   g.tab = c->tab;
@@ -763,7 +782,8 @@ int tcbee_owner_bucket_device(tcbee_ctx* c, uint32_t world, uint64_t seg_cap, ui
   if (!c || world == 0 || world > kMaxOwners || !seg_cap || !ent_dev || !lid_dev || !meta_dev)
     return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s;
+  TRY_HIP(ctx_stream(c, stream, s));
   if (int rc = apply_pending_reset(c, s)) return rc;
   TRY_HIP(hipMemsetAsync(meta_dev, 0, (world + 2ull) * sizeof(uint64_t), s));
   OwnerArgs a{};
@@ -785,7 +805,8 @@ int tcbee_status_raise_device(tcbee_ctx* c, const uint64_t* v_dev, uint64_t n, u
   if (!c || (n && !v_dev) || (n > 1 && !stride)) return TCBEE_EINVAL;
   if (!n) return TCBEE_OK;
   TRY_HIP(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s;
+  TRY_HIP(ctx_stream(c, stream, s));
   TRY_HIP(launch_status_raise(v_dev, n, stride, &c->d_persist->status, s));
   return TCBEE_OK;
 }
@@ -794,7 +815,8 @@ int tcbee_flow_first_seen_device(tcbee_ctx* c, uint64_t* out_dev, uint64_t cap, 
                                  void* stream) {
   if (!c || (cap && !out_dev)) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s;
+  TRY_HIP(ctx_stream(c, stream, s));
   if (int rc = apply_pending_reset(c, s)) return rc;
   TRY_HIP(launch_first_seen(c->tab, c->d_persist, out_dev, cap, n_dev, s));
   return TCBEE_OK;
@@ -947,7 +969,8 @@ int tcbee_flow_export_device(tcbee_ctx* c, tcbee_flow_entry* out_dev, uint64_t c
                              uint64_t* n_dev, void* stream) {
   if (!c || (cap && !out_dev)) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s;
+  TRY_HIP(ctx_stream(c, stream, s));
   TRY_HIP(k3_wait_stream(c, s));  // counters are K3's
   if (int rc = apply_pending_reset(c, s)) return rc;
   TRY_HIP(launch_export(c->tab, reinterpret_cast<uint64_t*>(out_dev), cap, c->d_persist, n_dev, s));
@@ -960,7 +983,8 @@ int tcbee_flow_export_global_device(tcbee_ctx* c, tcbee_flow_entry* out_dev, uin
                                     uint64_t rec_frame_cap, void* stream) {
   if (!c || (cap && !out_dev) || (n_frames && !frame_gidx_dev)) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s;
+  TRY_HIP(ctx_stream(c, stream, s));
   if (int rc = apply_pending_reset(c, s)) return rc;
   GlobalExportArgs g{};
   g.tab = c->tab;
@@ -984,7 +1008,8 @@ int tcbee_flow_records_before_device(tcbee_ctx* c, const uint32_t* rec_frame_dev
                                      void* stream) {
   if (!c || (cap && !out_counts_dev) || (n_rec_max && !frame_gidx_dev)) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s;
+  TRY_HIP(ctx_stream(c, stream, s));
   if (int rc = apply_pending_reset(c, s)) return rc;
   TRY_HIP(launch_records_before(c->tab, c->d_persist, rec_frame_dev, frame_gidx_dev, n_rec_dev,
                                 n_rec_max, out_counts_dev, cap, s));
@@ -995,7 +1020,8 @@ int tcbee_flow_set_first_seen_device(tcbee_ctx* c, const uint64_t* fs_by_id_dev,
                                      void* stream) {
   if (!c || (cap && !fs_by_id_dev)) return TCBEE_EINVAL;
   TRY_HIP(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s;
+  TRY_HIP(ctx_stream(c, stream, s));
   if (int rc = apply_pending_reset(c, s)) return rc;
   TRY_HIP(launch_set_first_seen(c->tab, c->d_persist, fs_by_id_dev, cap, s));
   return TCBEE_OK;
@@ -1010,7 +1036,8 @@ int tcbee_flow_merge_device(tcbee_ctx* c, const tcbee_flow_entry* ent_dev, uint6
   if (max_total_records >= (1ull << 31)) return TCBEE_ECAPACITY;
   const uint64_t total_records = max_total_records;
   TRY_HIP(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s;
+  TRY_HIP(ctx_stream(c, stream, s));
   const uint64_t words = (total_records + 31) / 32 + 1;
   if (!c->d_mcnt) TRY_HIP(dalloc(&c->d_mcnt, 2 * c->max_flows));
   if (words > c->m_words) {
@@ -1024,7 +1051,7 @@ int tcbee_flow_merge_device(tcbee_ctx* c, const tcbee_flow_entry* ent_dev, uint6
     c->d_mbprefix = nullptr;
     c->m_words = 0;
     TRY_HIP(dalloc(&c->d_mbitmap, words));
-    TRY_HIP(hipMemset(c->d_mbitmap, 0, words * sizeof(uint32_t)));  // cleared after each use
+    TRY_HIP(hipMemsetAsync(c->d_mbitmap, 0, words * sizeof(uint32_t), s));  // cleared after each use
     TRY_HIP(dalloc(&c->d_mwprefix, words));
     TRY_HIP(dalloc(&c->d_mbprefix, (words + kScanWordsPerBlock - 1) / kScanWordsPerBlock));
     c->m_words = words;
