@@ -601,6 +601,46 @@ def test_k3_chunk_sub_bin_boundaries(gpu, oracle, flows):
         assert p.status() == 0 and p.count_mode() == 1
 
 
+def test_null_stream_after_default_stream_work(gpu, oracle):
+    """A context created and used right behind work still queued on HIP's legacy
+    default stream (a framework's fills of the outputs, a busy default stream): with
+    a NULL stream the parse waits for that work (tcbee_amd.h), and the context's own
+    initialisation is complete when create returns. Outputs pre-filled with a
+    sentinel on the default stream; ids, records, counters and the table vs the
+    oracle. (A contract test: the round-5 failure this ordering fixed — every id 0,
+    about one parity-file run in five — was intermittent and this test alone passed
+    on the library before the fix too)"""
+    import torch
+    n, flows = 2_000_000, 150_000
+    tr = tcbee_amd.synth_trace(n, sizes="imix", kind=1, n_flows=flows, seed=77)
+    rec, fh, fi, ctr, table = oracle.parse(tr)
+    d_arena = torch.from_numpy(np.concatenate([tr.arena, np.zeros(64, np.uint8)])).cuda()
+    d_off = torch.from_numpy(tr.offset.view(np.int64)).cuda()
+    d_len = torch.from_numpy(tr.caplen.view(np.int32)).cuda()
+    d_ts = torch.from_numpy(tr.ts_ns.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    busy = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    for v in range(8):  # a few ms of default-stream work ahead of everything below
+        busy.fill_(v)
+    rec_d = torch.full((n * 74 + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+    fi_d = torch.full((n,), -2, dtype=torch.int32, device="cuda")
+    n_d = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctr_d = torch.zeros(4, dtype=torch.int64, device="cuda")
+    with tcbee_amd.PacketParser(max_frames=n, max_flows=flows + flows // 16) as p:
+        p.parse_device(d_arena, len(tr.arena), d_off, d_len, d_ts, n, rec_d, n, None, fi_d, n_d,
+                       ctr_d, stream=None)
+        p.sync()
+        torch.cuda.synchronize()
+        k = int(n_d.item())
+        assert k == len(rec)
+        assert np.array_equal(fi_d[:k].cpu().numpy().view(np.uint32), fi)
+        assert np.array_equal(rec_d[:k * 74].cpu().numpy().reshape(-1, 74), rec)
+        assert ctr_d.cpu().numpy().tolist() == [ctr["ingress"], ctr["egress"], ctr["handled"],
+                                                 ctr["dropped"]]
+        assert np.array_equal(p.flows(), table)
+    del busy
+
+
 @pytest.mark.parametrize("flows", [200_000, 1_000_000])
 def test_zipf_many_flows(gpu, oracle, flows):
     """Zipf(1.1) over many flows: a head flow holding ~12 % of the records beside a
