@@ -364,6 +364,14 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
             # whole table, the oracle fed the very frames the GPU parsed
             check.update(validate_shard_full(torch, d_arena, d_off, d_len, d_ts, last["rec"],
                                              last["hash"], last["id"], n, nrec, flows))
+        elif full_check and fx is not None:
+            # N>1: every rank checks ALL of its shard — records, hashes, global ids
+            # against a host recomputation of the global first-seen order, and its rows
+            # of the merged table (collective)
+            log(f"rank {rank}: full check of {n} shard records")
+            check.update(validate_shard_global(torch, dist, d_arena, d_off, d_len, d_ts,
+                                               last["rec"], last["hash"], last["id"], gidx, n,
+                                               nrec, flows))
         else:
             # every rank checks its own shard (global ids included) against the oracle
             check.update(validate_shard(torch, last["rec"], last["hash"], last["id"], gidx, n,
@@ -394,16 +402,25 @@ def all_ranks_check(torch, dist, check, status, n_local, n_global, flows, ctr):
     counters against the global frame count (every synthetic frame is accepted);
     the flow-hash shard imbalance (max / mean local frames), which bounds weak-scaling
     efficiency."""
-    ok = bool(check.get("sample_bit_exact", check.get("full_bit_exact", False))) and status == 0
+    full = "full_bit_exact" in check
+    ok = bool(check.get("full_bit_exact", check.get("sample_bit_exact", False))) and status == 0
+    if "merged_rows_exact" in check:
+        ok = ok and bool(check["merged_rows_exact"])
     v = torch.tensor([int(ok)], dtype=torch.int64, device="cuda")
     dist.all_reduce(v, op=dist.ReduceOp.MIN)
+    # every rank's own verdict and check kind, for the line (rank order)
+    flags = [torch.zeros(2, dtype=torch.int64, device="cuda") for _ in range(dist.get_world_size())]
+    dist.all_gather(flags, torch.tensor([int(ok), int(full)], dtype=torch.int64, device="cuda"))
     mx = torch.tensor([n_local], dtype=torch.int64, device="cuda")
     dist.all_reduce(mx, op=dist.ReduceOp.MAX)
     sm = torch.tensor([n_local], dtype=torch.int64, device="cuda")
     dist.all_reduce(sm)
     world = dist.get_world_size()
     mean = int(sm.item()) / world
+    per = [f.cpu().tolist() for f in flags]
     return {"all_ranks_bit_exact": bool(v.item()), "ranks_checked": world,
+            "ranks_full_bit_exact": [bool(a) and bool(b) for a, b in per],
+            "all_ranks_checked_in_full": all(bool(b) for _, b in per),
             "frames_local_max": int(mx.item()), "frames_local_mean": round(mean, 1),
             "shard_imbalance": round(int(mx.item()) / mean, 4) if mean else None,
             "global_frames_ok": int(sm.item()) == n_global,
@@ -481,6 +498,101 @@ def validate_shard_full(torch, d_arena, d_off, d_len, d_ts, d_rec, d_hash, d_id,
     table_ok = len(table) == len(gpu_flows) and np.array_equal(table, gpu_flows)
     out = {"full_bit_exact": bool(ok), "full_records": n, "flow_table_exact": bool(table_ok),
            "full_check_s": round(time.perf_counter() - t0, 1)}
+    if bad_at is not None:
+        out["first_bad_chunk"] = bad_at
+    return out
+
+
+def validate_shard_global(torch, dist, d_arena, d_off, d_len, d_ts, d_rec, d_hash, d_id, gidx,
+                          n, nrec, merged_flows, chunk=2_000_000):
+    """N>1 flow-hash shards, checked IN FULL on every rank (collective):
+      1. every record and flow hash of this rank's shard vs the oracle run over the
+         SAME frames (copied back from the device arena chunk by chunk, one oracle flow
+         table carried across the chunks) — the oracle's shard-local ids are kept;
+      2. the GLOBAL ids, against an independent host recomputation of the global
+         first-seen order: each local flow's first global frame (the oracle table's
+         first record -> gidx) is all-gathered over the ranks (padded to the largest
+         rank's flow count), numpy sorts the union, and a flow's global id is its rank
+         in that order; every device id of the shard must equal
+         global_id[oracle local id]. No device exchange output is used;
+      3. the merged global table (FlowHashExchange.merged_flows, identical on every
+         rank): this rank's flows' rows — tuple, pkts, bytes, first_seen = global
+         record index (every synthetic frame is accepted: = the first global frame) —
+         against its oracle table, and the merged flow count against the union's.
+    Host memory: 4 B per local record of oracle ids, kept between passes."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_py import Oracle
+    from tcbee_amd.trace import Trace
+    orc = Oracle()
+    ft = orc.new_flowtab(1 << 18)
+    t0 = time.perf_counter()
+    rec_ok = nrec == n
+    bad_at = None
+    fi_local = np.empty(n, dtype=np.uint32)
+    g_host = gidx[:n].cpu().numpy().astype(np.int64)
+    try:
+        for lo in range(0, n, chunk):
+            hi = min(n, lo + chunk)
+            off = d_off[lo:hi].cpu().numpy().view(np.uint64)
+            ln = d_len[lo:hi].cpu().numpy().view(np.uint32)
+            a0, a1 = int(off[0]), int(off[-1]) + int(ln[-1])
+            arena = d_arena[a0:a1].cpu().numpy()
+            tr = Trace(arena, (off - np.uint64(a0)).astype(np.uint64), ln.copy(),
+                       d_ts[lo:hi].cpu().numpy().view(np.uint64).copy())
+            rec, fh, fi, _, _ = orc.parse(tr, ft=ft, record_base=lo)
+            same = (len(rec) == hi - lo
+                    and np.array_equal(d_rec[lo * 74: hi * 74].cpu().numpy().reshape(-1, 74), rec)
+                    and np.array_equal(d_hash[lo:hi].cpu().numpy().view(np.uint32), fh))
+            if len(fi) == hi - lo:
+                fi_local[lo:hi] = fi
+            if not same and bad_at is None:
+                bad_at = lo
+            rec_ok = rec_ok and same
+            if (lo // chunk) % 10 == 9:
+                log(f"shard check: {hi}/{n} records ({time.perf_counter() - t0:.0f}s)")
+        table = orc.flows(ft)
+    finally:
+        orc.free_flowtab(ft)
+    # global first-seen order from the ranks' oracle tables (host recomputation)
+    nloc = len(table)
+    first_g = g_host[table["first_seen"].astype(np.int64)] if nloc else np.zeros(0, np.int64)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    cnt = torch.tensor([nloc], dtype=torch.int64, device=dev)
+    cnts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt)
+    cnts = [int(c.item()) for c in cnts]
+    pad = max(max(cnts), 1)
+    mine = torch.full((pad,), -1, dtype=torch.int64, device=dev)
+    mine[:nloc] = torch.from_numpy(first_g)
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine)
+    allf = np.concatenate([parts[r][:cnts[r]].cpu().numpy() for r in range(world)])
+    order = np.argsort(allf, kind="stable")
+    gid_all = np.empty(len(allf), dtype=np.int64)
+    gid_all[order] = np.arange(len(allf))
+    base = sum(cnts[:rank])
+    gid = gid_all[base:base + nloc]
+    distinct = len(np.unique(allf)) == len(allf)  # flows of disjoint shards: distinct frames
+    ids_ok = rec_ok and distinct
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        want = gid[fi_local[lo:hi].astype(np.int64)].astype(np.uint32) if nloc else \
+            np.zeros(hi - lo, np.uint32)
+        ids_ok = ids_ok and np.array_equal(d_id[lo:hi].cpu().numpy().view(np.uint32), want)
+    # this rank's rows of the merged global table
+    mf = merged_flows
+    table_ok = len(mf) == len(allf) and nloc > 0
+    if table_ok:
+        rows = mf[gid]
+        table_ok = (np.array_equal(rows["tuple"], table["tuple"])
+                    and np.array_equal(rows["pkts"], table["pkts"])
+                    and np.array_equal(rows["bytes"], table["bytes"])
+                    and np.array_equal(rows["first_seen"].astype(np.int64), first_g))
+    out = {"full_bit_exact": bool(rec_ok and ids_ok), "full_records": n,
+           "records_hashes_exact": bool(rec_ok), "global_ids_exact": bool(ids_ok),
+           "merged_rows_exact": bool(table_ok), "flows_local": nloc,
+           "flows_global_recomputed": len(allf), "full_check_s": round(time.perf_counter() - t0, 1)}
     if bad_at is not None:
         out["first_bad_chunk"] = bad_at
     return out
@@ -589,6 +701,11 @@ def cpu_baseline(sizes, kind, n_flows, seed, seconds, threads, sample_n=2_000_00
     return out, tr.n
 
 
+def _lib_identity() -> dict:
+    from tcbee_amd import _lib
+    return _lib.lib_identity()
+
+
 def host_cores() -> int:
     """The host cores this job may use: what `nproc` prints (coreutils honours
     OMP_NUM_THREADS, which the GPU box sets to the job's CPU share, 16 per GPU;
@@ -669,6 +786,7 @@ def host_e2e(sizes, kind, n_flows, seed, n=20_000_000, reps=9, threads=None):
             if ref is None:
                 ref = (rec_out.copy(), id_out.copy())
             if mode == "auto":
+                p.reset_flows()  # (calibrate_output refuses a pipe that holds flows)
                 out["calibration"] = p.calibrate_output(tr, frames=4_000_000, reps=2)
             ts[name] = []
         log(f"e2e: {reps} interleaved rounds")
@@ -877,7 +995,7 @@ def main():
         log(f"rank {rank}: config-4 leg ({args.c4_frames} frames per GPU, 1M flows)")
         c_el, c_k1, c_n, c_chk, c_local = run_device(
             torch, dist, rank, world, args.c4_frames, "imix", 1, 1_000_000, args.c4_steps, 1,
-            args.seed, multi=True, flowhash=True)
+            args.seed, multi=True, flowhash=True, full_check=not args.sample_check)
         c_el = max_over_ranks(torch, dist, c_el)
         c4 = {"workload": "config4: IMIX 64/576/1500 7:4:1 IPv4/TCP, 1000000 flows, "
                           "flow-hash shards, FlowHashExchange",
@@ -918,6 +1036,9 @@ def main():
                          "k1_ms": round(k1_ms, 4),
                          "alg_bytes_per_frame": IDX_BYTES + hdr + OUT_BYTES},
             "check": check,
+            # the binary measured: path + sha256 prefix of the libtcbee_amd.so this process
+            # loaded (TCBEE_AB_LIB swaps it only with TCBEE_AB_OPTIN=1: then ab_lib is true)
+            **_lib_identity(),
         }
         if dist is not None:
             out["dist"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size()}

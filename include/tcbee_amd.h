@@ -509,9 +509,13 @@ int tcbee_pipe_run(tcbee_pipe* p, const tcbee_frames* in_host, const tcbee_cfg* 
  * out_cap still goes through staging. The sink then receives pointers into the
  * caller's arrays. out_flow_id may be NULL (records only). Registering another
  * pair (or NULL, 0, NULL) releases the previous one; tcbee_pipe_destroy releases
- * it too. The caller keeps the arrays alive while registered. An array already
- * page-locked (by another pipe, or by the caller's hipHostRegister) is used as it
- * is and left page-locked on release, so several pipes may share one pair. */
+ * it too. The caller keeps the arrays alive while registered. Several pipes may
+ * share one pair: a range another pipe page-locked is borrowed when that
+ * registration covers the requested bytes (refcounted, process-wide; the range is
+ * unregistered when its last holder releases it, whichever pipe locked it), a
+ * range overlapping a registration without lying inside it is TCBEE_EINVAL; a
+ * range the caller page-locked itself is used as it is when both of its ends are
+ * registered (else TCBEE_EINVAL) and never unregistered here. */
 int tcbee_pipe_register_output(tcbee_pipe* p, uint8_t* out_rec74, uint64_t cap,
                                uint32_t* out_flow_id);
 

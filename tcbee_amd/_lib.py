@@ -19,9 +19,16 @@ LIB_PATH = os.path.join(_HERE, "lib", "libtcbee_amd.so")
 VARIANTS_LIB_PATH = os.path.join(_HERE, "lib", "libtcbee_amd_variants.so")
 # A/B tooling only (tools/lib_ab.sh: the same workload against an older build of the
 # kernels, or the variants build, in another process); the product and the tests
-# load the in-tree library
+# load the in-tree library. The swap needs an explicit second opt-in
+# (TCBEE_AB_OPTIN=1, set by the A/B scripts): a stray TCBEE_AB_LIB alone must not
+# silently replace the product under a bench or a test.
+AB_LIB = None
 if os.environ.get("TCBEE_AB_LIB"):
-    LIB_PATH = os.path.abspath(os.environ["TCBEE_AB_LIB"])
+    if os.environ.get("TCBEE_AB_OPTIN") != "1":
+        raise ImportError("TCBEE_AB_LIB is set without TCBEE_AB_OPTIN=1: refusing to load "
+                          f"{os.environ['TCBEE_AB_LIB']} in place of the product library "
+                          "(A/B tooling sets both; unset TCBEE_AB_LIB otherwise)")
+    AB_LIB = LIB_PATH = os.path.abspath(os.environ["TCBEE_AB_LIB"])
 
 RECORD_BYTES = 74
 TRACE_BYTES = 72
@@ -204,6 +211,14 @@ _SIGS = {
                                  C.POINTER(C.c_uint64), C.POINTER(Counters)]),
 }
 EXPORTED = tuple(_SIGS)
+# test entry points of the variants build only (not in include/tcbee_amd.h)
+_VARIANT_SIGS = {
+    "tcbee_test_flag_create": (C.c_int, [C.POINTER(C.c_void_p)]),
+    "tcbee_test_flag_destroy": (C.c_int, [C.c_void_p]),
+    "tcbee_test_wait_host_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
+                                              C.c_void_p]),
+    "tcbee_test_k2_hold": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+}
 
 _libs: dict = {}
 
@@ -220,15 +235,29 @@ def lib(variants: bool = False) -> C.CDLL:
                 "or __graft_entry__.build() (no CPU fallback exists)")
         _share_hip_runtime_with_torch()
         L = C.CDLL(path)
-        for name, (res, args) in _SIGS.items():
+        sigs = dict(_SIGS, **_VARIANT_SIGS) if variants else _SIGS
+        for name, (res, args) in sigs.items():
             # (an older build under TCBEE_AB_LIB may predate some entry points)
-            if os.environ.get("TCBEE_AB_LIB") and not hasattr(L, name):
+            if (AB_LIB or variants) and not hasattr(L, name):
                 continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
         _libs[path] = L
     return L
+
+
+def lib_identity(variants: bool = False) -> dict:
+    """Path and sha256 prefix of the library lib(variants) loads (the bench line
+    records which binary it measured)."""
+    import hashlib
+    path = VARIANTS_LIB_PATH if variants else LIB_PATH
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return {"lib_path": os.path.relpath(path, os.path.dirname(_HERE)) if not AB_LIB else path,
+            "lib_sha256_16": h.hexdigest()[:16], "ab_lib": bool(AB_LIB)}
 
 
 def _share_hip_runtime_with_torch() -> None:

@@ -32,6 +32,15 @@ struct tcbee_ctx {
   uint32_t plain_walk = kPlainWalk;  // TCBEE_WALK: K1 plain probe walk length (test hook:
                                      // 0 sends every foreign slot to the coherent path)
   bool no_fuse_rank = false;         // TCBEE_NO_FUSE_RANK: the separate rank launch (A/B, tests)
+  // TCBEE_TEST_LEGACY_INIT (test hook, variants build only): the creation path of
+  // rounds 1-5 before bccf225 — creation-time memsets through hipMemset on HIP's legacy
+  // default stream, and a NULL-stream call NOT ordered after that stream — so a test
+  // can reproduce the round-5 all-zero-id race on purpose
+  bool legacy_init = false;
+#if TCBEE_VARIANTS
+  const uint64_t* test_hold = nullptr;  // tcbee_test_k2_hold
+  uint64_t* test_hold_state = nullptr;
+#endif
   uint32_t pack_bits = 0;            // K1->K3 scratch packing (0: two words per record)
 
   FlowTable tab{};
@@ -114,15 +123,30 @@ struct tcbee_ctx {
 // ordered after whatever is already queued on the legacy default stream (a caller's
 // default-stream producers of the inputs, or zero-fills of the outputs, would
 // otherwise race the parse: the context's stream does not wait for that stream).
+// The context's device is made current first (the legacy stream recorded
+// below is the CURRENT device's, so a thread driving several GPUs must not record
+// another device's default stream into ev_null).
 static hipError_t ctx_stream(tcbee_ctx* c, void* stream, hipStream_t& s) {
+  if (hipError_t e = hipSetDevice(c->device); e != hipSuccess) return e;
   if (stream) {
     s = (hipStream_t)stream;
     return hipSuccess;
   }
   s = c->stream;
+  if (c->legacy_init) return hipSuccess;  // (test hook: the unordered pre-fix path)
   hipError_t e = hipEventRecord(c->ev_null, nullptr);
   if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_null, 0);
   return e;
+}
+// Creation-time fills: on the context's stream (create synchronizes it before it
+// returns), or under the legacy-init test hook on the legacy default stream as the
+// pre-fix code did.
+static hipError_t init_fill(tcbee_ctx* c, void* p, int v, size_t bytes) {
+  return c->legacy_init ? hipMemset(p, v, bytes) : hipMemsetAsync(p, v, bytes, c->stream);
+}
+static hipError_t init_fill_2d(tcbee_ctx* c, void* p, size_t pitch, int v, size_t w, size_t h) {
+  return c->legacy_init ? hipMemset2D(p, pitch, v, w, h)
+                        : hipMemset2DAsync(p, pitch, v, w, h, c->stream);
 }
 static constexpr uint64_t kMaxProfiled = 4096;
 
@@ -307,6 +331,7 @@ int tcbee_ctx_create_ex(tcbee_ctx** out, int device, uint64_t max_frames, uint64
   if (const char* e = std::getenv("TCBEE_TEST_K3_WIDE")) c->k3_wide = std::atoi(e) != 0;
   if (const char* e = std::getenv("TCBEE_WALK")) c->plain_walk = (uint32_t)std::atoi(e);
   if (const char* e = std::getenv("TCBEE_NO_FUSE_RANK")) c->no_fuse_rank = std::atoi(e) != 0;
+  if (const char* e = std::getenv("TCBEE_TEST_LEGACY_INIT")) c->legacy_init = std::atoi(e) != 0;
   if (const char* e = std::getenv("TCBEE_FPL")) {
     const int v = std::atoi(e);
     if (v == 1 || v == 2 || v == 4) c->fpl = v;
@@ -355,10 +380,10 @@ int tcbee_ctx_create_ex(tcbee_ctx** out, int device, uint64_t max_frames, uint64
   if ((e = dalloc(&c->tab.wide, 8 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
   // all ones, then every tag word zero (k_table_init sweeps the wide slots only once
   // used): fs words ~0 as a reset leaves them
-  if ((e = hipMemsetAsync(c->tab.wide, 0xFF, 64 * (c->tab.wide_mask + 1), c->stream)) != hipSuccess) return fail(map_err(e));
-  if ((e = hipMemset2DAsync(c->tab.wide, 64, 0, 8, c->tab.wide_mask + 1, c->stream)) != hipSuccess) return fail(map_err(e));
+  if ((e = init_fill(c, c->tab.wide, 0xFF, 64 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
+  if ((e = init_fill_2d(c, c->tab.wide, 64, 0, 8, c->tab.wide_mask + 1)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.wide_used, 1)) != hipSuccess) return fail(map_err(e));
-  if ((e = hipMemsetAsync(c->tab.wide_used, 0, 4, c->stream)) != hipSuccess) return fail(map_err(e));
+  if ((e = init_fill(c, c->tab.wide_used, 0, 4)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.cnt, 2 * c->max_flows)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->tab.cmap, c->max_flows)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_persist, 1)) != hipSuccess) return fail(map_err(e));
@@ -369,12 +394,12 @@ int tcbee_ctx_create_ex(tcbee_ctx** out, int device, uint64_t max_frames, uint64
       return fail(map_err(e));
   if ((e = dalloc(&c->d_tile_status, c->max_tiles)) != hipSuccess) return fail(map_err(e));
   // all zero between batches of small contexts (their K3 re-zeroes the words a batch used)
-  if ((e = hipMemsetAsync(c->d_tile_status, 0, c->max_tiles * sizeof(uint64_t), c->stream)) != hipSuccess)
+  if ((e = init_fill(c, c->d_tile_status, 0, c->max_tiles * sizeof(uint64_t))) != hipSuccess)
     return fail(map_err(e));
   if ((e = dalloc(&c->d_new_list, c->max_flows)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_bitmap, c->max_words)) != hipSuccess) return fail(map_err(e));
   // all zero between batches from here on (K3 clears the words a batch set)
-  if ((e = hipMemsetAsync(c->d_bitmap, 0, c->max_words * sizeof(uint32_t), c->stream)) != hipSuccess)
+  if ((e = init_fill(c, c->d_bitmap, 0, c->max_words * sizeof(uint32_t))) != hipSuccess)
     return fail(map_err(e));
   if ((e = dalloc(&c->d_wprefix, c->max_words)) != hipSuccess) return fail(map_err(e));
   if ((e = dalloc(&c->d_bprefix, c->max_sblocks)) != hipSuccess) return fail(map_err(e));
@@ -435,13 +460,13 @@ int tcbee_ctx_create_ex(tcbee_ctx** out, int device, uint64_t max_frames, uint64
     c->tab_alt.cnt = nullptr;
     if ((e = dalloc(&c->tab_alt.slots, 8 * c->nlines)) != hipSuccess) return fail(map_err(e));
     if ((e = dalloc(&c->tab_alt.wide, 8 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
-    if ((e = hipMemsetAsync(c->tab_alt.wide, 0xFF, 64 * (c->tab.wide_mask + 1), c->stream)) != hipSuccess) return fail(map_err(e));
-    if ((e = hipMemset2DAsync(c->tab_alt.wide, 64, 0, 8, c->tab.wide_mask + 1, c->stream)) != hipSuccess) return fail(map_err(e));
+    if ((e = init_fill(c, c->tab_alt.wide, 0xFF, 64 * (c->tab.wide_mask + 1))) != hipSuccess) return fail(map_err(e));
+    if ((e = init_fill_2d(c, c->tab_alt.wide, 64, 0, 8, c->tab.wide_mask + 1)) != hipSuccess) return fail(map_err(e));
     if ((e = dalloc(&c->tab_alt.wide_used, 1)) != hipSuccess) return fail(map_err(e));
-    if ((e = hipMemsetAsync(c->tab_alt.wide_used, 0, 4, c->stream)) != hipSuccess) return fail(map_err(e));
+    if ((e = init_fill(c, c->tab_alt.wide_used, 0, 4)) != hipSuccess) return fail(map_err(e));
     if ((e = dalloc(&c->tab_alt.cnt, 2 * c->max_flows)) != hipSuccess) return fail(map_err(e));
     if ((e = dalloc(&c->d_persist_alt, 1)) != hipSuccess) return fail(map_err(e));
-    if ((e = hipMemsetAsync(c->d_persist_alt, 0, sizeof(PersistState), c->stream)) != hipSuccess) return fail(map_err(e));
+    if ((e = init_fill(c, c->d_persist_alt, 0, sizeof(PersistState))) != hipSuccess) return fail(map_err(e));
     if ((e = launch_table_init(c->tab_alt, c->stream)) != hipSuccess) return fail(map_err(e));
     if ((e = dalloc(&c->d_batch_slot[1], 1)) != hipSuccess) return fail(map_err(e));
     if ((e = dalloc(&c->d_slot_scratch_s[1], c->max_frames)) != hipSuccess) return fail(map_err(e));
@@ -524,8 +549,7 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     return TCBEE_EINVAL;
   const bool flows = (cfg->flags & TCBEE_F_NO_FLOWS) == 0;
   hipStream_t s;
-  TRY_HIP(ctx_stream(c, stream, s));
-  TRY_HIP(hipSetDevice(c->device));
+  TRY_HIP(ctx_stream(c, stream, s));  // (sets c->device current)
   if (async && c->nslot < 2) {
     // first async batch: the second slot (setup, synchronous allocation)
     TRY_HIP(dalloc(&c->d_batch_slot[1], 1));
@@ -625,6 +649,10 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     r.nwords = nwords;
     r.nblocks = (r.nwords + kScanWordsPerBlock - 1) / kScanWordsPerBlock;
     r.update_persist = true;
+#if TCBEE_VARIANTS
+    r.test_hold = c->test_hold;
+    r.test_hold_state = c->test_hold_state;
+#endif
     // K2 rewrites claim -> id entries, zeroes new ids' counters and the bitmap K3
     // clears: after the previous batch's K3, wherever that ran
     TRY_HIP(k3_wait_stream(c, s));
@@ -1051,9 +1079,13 @@ int tcbee_flow_merge_device(tcbee_ctx* c, const tcbee_flow_entry* ent_dev, uint6
     c->d_mbprefix = nullptr;
     c->m_words = 0;
     TRY_HIP(dalloc(&c->d_mbitmap, words));
-    TRY_HIP(hipMemsetAsync(c->d_mbitmap, 0, words * sizeof(uint32_t), s));  // cleared after each use
     TRY_HIP(dalloc(&c->d_mwprefix, words));
     TRY_HIP(dalloc(&c->d_mbprefix, (words + kScanWordsPerBlock - 1) / kScanWordsPerBlock));
+    // all zero between merges from here on (each merge clears the words it set); the
+    // fill completes before this call returns, so a later merge on any
+    // stream finds it done
+    TRY_HIP(hipMemsetAsync(c->d_mbitmap, 0, words * sizeof(uint32_t), c->stream));
+    TRY_HIP(hipStreamSynchronize(c->stream));
     c->m_words = words;
   }
   // fresh table: the merge result replaces whatever this context held
@@ -1286,3 +1318,44 @@ uint64_t tcbee_flow_hash64(const uint8_t key[TCBEE_KEY_BYTES]) {
 }
 
 }  // extern "C"
+
+#if TCBEE_VARIANTS
+// ---- test entry points of the variants build (not in include/tcbee_amd.h) ----
+// The race test of DESIGN.md section 6 (round 6): host-released waits
+// that pin an interleaving of the legacy default stream and a context's stream.
+extern "C" {
+// A page-locked, coherent host word (0), readable by kernels; the test stores to it.
+int tcbee_test_flag_create(uint64_t** host_flag) {
+  if (!host_flag) return TCBEE_EINVAL;
+  TRY_HIP(hipHostMalloc(reinterpret_cast<void**>(host_flag), 64,
+                        hipHostMallocMapped | hipHostMallocCoherent));
+  **host_flag = 0;
+  return TCBEE_OK;
+}
+int tcbee_test_flag_destroy(uint64_t* host_flag) {
+  if (host_flag) TRY_HIP(hipHostFree(host_flag));
+  return TCBEE_OK;
+}
+// Queue a wait on `stream` (NULL: HIP's legacy default stream) until *host_flag ==
+// expect; wall-clock bounded (timeout_us). *state_dev = 3 released, 1 timed out.
+int tcbee_test_wait_host_device(uint64_t* host_flag, uint64_t expect, uint64_t timeout_us,
+                                uint64_t* state_dev, void* stream) {
+  if (!host_flag || !state_dev) return TCBEE_EINVAL;
+  void* dflag = nullptr;
+  TRY_HIP(hipHostGetDevicePointer(&dflag, host_flag, 0));
+  TRY_HIP(launch_test_wait_host(static_cast<const uint64_t*>(dflag), expect, timeout_us,
+                                state_dev, (hipStream_t)stream));
+  return TCBEE_OK;
+}
+// Every later batch of `c` that ranks with the four-kernel K2 holds its stream between
+// k_mark and k_scan_words until *host_flag == 1 (NULL: off).
+int tcbee_test_k2_hold(tcbee_ctx* c, uint64_t* host_flag, uint64_t* state_dev) {
+  if (!c || (host_flag && !state_dev)) return TCBEE_EINVAL;
+  void* dflag = nullptr;
+  if (host_flag) TRY_HIP(hipHostGetDevicePointer(&dflag, host_flag, 0));
+  c->test_hold = static_cast<const uint64_t*>(dflag);
+  c->test_hold_state = state_dev;
+  return TCBEE_OK;
+}
+}  // extern "C"
+#endif

@@ -147,12 +147,24 @@ struct RankArgs {
   bool update_persist;  // parse (not merge): advance rec_base / flow_count when
                         // done and zero the new ids' counters, so the batch's K3
                         // may run on another stream beside the next batch's K1
+#if TCBEE_VARIANTS
+  // test hook (tcbee_test_k2_hold): hold the stream between k_mark and k_scan_words
+  // until a host-written flag reads 1 (the race test of DESIGN.md section 6)
+  const uint64_t* test_hold = nullptr;
+  uint64_t* test_hold_state = nullptr;
+#endif
 };
 
 // Launchers (tcbee_kernels.hip). All asynchronous on `s`.
 hipError_t launch_table_init(FlowTable t, hipStream_t s);
 hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s);
 hipError_t launch_rank(const RankArgs& r, hipStream_t s);
+#if TCBEE_VARIANTS
+// test hook: one lane holds `s` until *flag_dev == expect (a page-locked coherent host
+// word, system-scope loads) or timeout_us pass; *state = 3 released, 1 timed out
+hipError_t launch_test_wait_host(const uint64_t* flag_dev, uint64_t expect, uint64_t timeout_us,
+                                 uint64_t* state, hipStream_t s);
+#endif
 struct CountArgs {
   uint64_t* out_n;           // finalize (block 0): record count, counters, running bases
   tcbee_counters* ctr;

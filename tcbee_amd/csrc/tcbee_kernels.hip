@@ -2066,12 +2066,42 @@ hipError_t launch_prep(const PrepArgs& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+#if TCBEE_VARIANTS
+__global__ void k_test_wait_host(const uint64_t* flag, uint64_t expect, int64_t timeout_ticks,
+                                 uint64_t* state) {
+  if (threadIdx.x != 0) return;
+  const int64_t t0 = wall_clock64();
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != expect) {
+    if (wall_clock64() - t0 > timeout_ticks) {
+      *state = 1;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+  *state = 3;
+}
+
+hipError_t launch_test_wait_host(const uint64_t* flag_dev, uint64_t expect, uint64_t timeout_us,
+                                 uint64_t* state, hipStream_t s) {
+  // (wall_clock64 ticks at 100 MHz on MI355X)
+  hipLaunchKernelGGL(k_test_wait_host, dim3(1), dim3(64), 0, s, flag_dev, expect,
+                     (int64_t)(timeout_us * 100), state);
+  return hipGetLastError();
+}
+#endif
+
 hipError_t launch_rank(const RankArgs& r, hipStream_t s) {
   if (r.nwords <= kRankSmallWords) {
     hipLaunchKernelGGL(k_rank_small, dim3(1), dim3(1024), 0, s, r);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_mark, dim3(1024), dim3(kBlock), 0, s, r);
+#if TCBEE_VARIANTS
+  if (r.test_hold) {
+    const hipError_t e = launch_test_wait_host(r.test_hold, 1, 10'000'000, r.test_hold_state, s);
+    if (e != hipSuccess) return e;
+  }
+#endif
   hipLaunchKernelGGL(k_scan_words, dim3((unsigned)(r.nblocks < 512 ? r.nblocks : 512)), dim3(kBlock),
                      0, s, r);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kBlock), 0, s, r);

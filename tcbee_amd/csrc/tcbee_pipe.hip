@@ -70,6 +70,7 @@ int map_err(hipError_t e) {
   if (e == hipSuccess) return TCBEE_OK;
   if (e == hipErrorOutOfMemory) return TCBEE_ENOMEM;
   if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return TCBEE_ENODEV;
+  if (e == hipErrorInvalidValue) return TCBEE_EINVAL;
   return TCBEE_EDEVICE;
 }
 
@@ -188,8 +189,7 @@ struct tcbee_pipe {
   uint8_t* reg_rec = nullptr;
   uint32_t* reg_id = nullptr;
   uint64_t reg_cap = 0;
-  bool own_rec = false, own_id = false;  // page-locked by this pipe (else borrowed:
-                                         // already registered when it was handed in)
+  uint64_t reg_rec_bytes = 0, reg_id_bytes = 0;  // the ranges held in the registry
   uint64_t prefetch = 48;  // header-window gather: frames ahead (TCBEE_PIPE_PF, 0 = off)
   int nt_copy = 1;         // header-window gather: fixed-size 16-B loads + streaming
                            // stores into the staging (TCBEE_PIPE_NT=0: memcpy)
@@ -197,30 +197,74 @@ struct tcbee_pipe {
 
 namespace {
 
-void unregister_output(tcbee_pipe* p) {
-  if (p->reg_rec && p->own_rec) (void)hipHostUnregister(p->reg_rec);
-  if (p->reg_id && p->own_id) (void)hipHostUnregister(p->reg_id);
-  (void)hipGetLastError();  // (a failed release must not surface in a later call)
-  p->reg_rec = nullptr;
-  p->reg_id = nullptr;
-  p->reg_cap = 0;
-  p->own_rec = p->own_id = false;
-}
+// Page-locked output ranges, process-wide: pipes handed the same arrays
+// share ONE registration. An entry is the range some pipe page-locked with
+// hipHostRegister, and the pipes holding it; a pipe borrows an entry only when the
+// entry covers the bytes it asks for, and the range is unregistered when its LAST
+// holder releases it. Every holder syncs its own D2H stream before it releases
+// (register_output, free_pipe), so by then no holder's D2H into the range is in
+// flight — the owner can be released first without pulling the pages from under a
+// borrower. A range the CALLER page-locked (not in the registry) is used as is when
+// both of its ends are registered, and never unregistered here.
+struct HostReg {
+  uint8_t* base;
+  uint64_t bytes;
+  uint32_t holders;
+};
+std::mutex g_reg_mu;
+std::vector<HostReg> g_regs;
 
-// hipHostRegister, or nothing when the range is page-locked already (by another
-// pipe or by the caller): then it is borrowed and left registered on release. (The
-// state is queried first: a second hipHostRegister of a registered range made the
-// owner's later hipHostUnregister fail.)
-hipError_t register_range(void* ptr, uint64_t bytes, bool& own) {
+hipError_t register_range(void* ptr, uint64_t bytes) {
+  uint8_t* const b = static_cast<uint8_t*>(ptr);
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  for (HostReg& r : g_regs) {
+    if (b >= r.base && b + bytes <= r.base + r.bytes) {
+      ++r.holders;
+      return hipSuccess;
+    }
+    if (b < r.base + r.bytes && r.base < b + bytes)
+      return hipErrorInvalidValue;  // overlaps a registration without being inside it
+  }
   unsigned int flags = 0;
   if (hipHostGetFlags(&flags, ptr) == hipSuccess) {
-    own = false;
+    // page-locked by the caller: borrow it if it reaches the last byte too
+    if (hipHostGetFlags(&flags, b + bytes - 1) != hipSuccess) {
+      (void)hipGetLastError();
+      return hipErrorInvalidValue;
+    }
     return hipSuccess;
   }
   (void)hipGetLastError();  // (pageable: the query's error is expected)
   const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
-  own = e == hipSuccess;
+  if (e == hipSuccess) g_regs.push_back({b, bytes, 1});
   return e;
+}
+
+void release_range(void* ptr, uint64_t bytes) {
+  uint8_t* const b = static_cast<uint8_t*>(ptr);
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  for (size_t i = 0; i < g_regs.size(); ++i) {
+    HostReg& r = g_regs[i];
+    if (b >= r.base && b + bytes <= r.base + r.bytes) {
+      if (--r.holders == 0) {
+        (void)hipHostUnregister(r.base);
+        (void)hipGetLastError();  // (a failed release must not surface in a later call)
+        g_regs.erase(g_regs.begin() + i);
+      }
+      return;
+    }
+  }
+  // not in the registry: the caller's own registration, left as it was
+}
+
+// (the pipe's D2H stream must be idle: callers sync it first)
+void unregister_output(tcbee_pipe* p) {
+  if (p->reg_rec && p->reg_rec_bytes) release_range(p->reg_rec, p->reg_rec_bytes);
+  if (p->reg_id && p->reg_id_bytes) release_range(p->reg_id, p->reg_id_bytes);
+  p->reg_rec = nullptr;
+  p->reg_id = nullptr;
+  p->reg_cap = 0;
+  p->reg_rec_bytes = p->reg_id_bytes = 0;
 }
 
 void free_pipe(tcbee_pipe* p) {
@@ -490,15 +534,17 @@ int tcbee_pipe_register_output(tcbee_pipe* p, uint8_t* out_rec74, uint64_t cap,
   TRY_HIP(hipStreamSynchronize(p->s_d2h));  // no D2H into the old arrays in flight
   unregister_output(p);
   if (!cap) return TCBEE_OK;
-  TRY_HIP(register_range(out_rec74, cap * TCBEE_RECORD_BYTES, p->own_rec));
+  TRY_HIP(register_range(out_rec74, cap * TCBEE_RECORD_BYTES));
   p->reg_rec = out_rec74;
+  p->reg_rec_bytes = cap * TCBEE_RECORD_BYTES;
   if (out_flow_id) {
-    const hipError_t e = register_range(out_flow_id, cap * 4, p->own_id);
+    const hipError_t e = register_range(out_flow_id, cap * 4);
     if (e != hipSuccess) {
       unregister_output(p);
       return map_err(e);
     }
     p->reg_id = out_flow_id;
+    p->reg_id_bytes = cap * 4;
   }
   p->reg_cap = cap;
   return TCBEE_OK;

@@ -16,6 +16,7 @@ per-rank tables merged here.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import shutil
 import time
@@ -32,6 +33,32 @@ ENTRY_WORDS = 8  # tcbee_flow_entry = 64 B = u64[8]
 def shard_range(n_total: int, rank: int, world: int) -> tuple[int, int]:
     """Frames [lo, hi) of rank `rank`: contiguous, sizes differ by at most one."""
     return n_total * rank // world, n_total * (rank + 1) // world
+
+
+@contextlib.contextmanager
+def rank_stream(parser: "_parser.PacketParser", stream: int | None):
+    """The ONE stream a step's device calls AND its collectives run on.
+
+    The C ABI reads a NULL stream as the context's own non-blocking stream, while
+    torch issues RCCL / gloo collectives and tensor ops on its CURRENT stream; with
+    torch's default stream (handle 0) the two differ, so a collective could read
+    `first` / `ctr` before the kernels writing them ran. Here:
+      * `stream` is torch's current stream: used as is (the caller's contract);
+      * `stream` is 0 / None: the context's stream, made torch's current stream for
+        the step (collectives included) after waiting for the caller's current
+        stream (its producers of the inputs), and the caller's stream waits for it on
+        exit (its readers of the outputs);
+      * any other handle: the same, on that stream.
+    Yields the handle to pass to every device call of the step."""
+    cur = torch.cuda.current_stream()
+    if stream and int(stream) == cur.cuda_stream:
+        yield int(stream)
+        return
+    tgt = torch.cuda.ExternalStream(int(stream) if stream else parser.stream, device=cur.device)
+    tgt.wait_stream(cur)
+    with torch.cuda.stream(tgt):
+        yield tgt.cuda_stream
+    cur.wait_stream(tgt)
 
 
 def all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
@@ -116,39 +143,43 @@ class FlowMerge:
         first record: via rec_frame (the parse's out_frame, rec_cap entries) or,
         without it, assuming every frame was accepted (checked on the device:
         otherwise the local context's status reports TCBEE_ESHARD)."""
-        if self.gidx is None:
-            self.local.export_device(self.ent[slot], self.cap, self.meta[slot], stream=stream)
-        else:
-            self.local.export_global_device(self.ent[slot], self.cap, self.meta[slot],
-                                            self.gidx, self.gidx.numel(), rec_frame=rec_frame,
-                                            rec_frame_cap=rec_cap, stream=stream)
+        with rank_stream(self.local, stream) as s:
+            if self.gidx is None:
+                self.local.export_device(self.ent[slot], self.cap, self.meta[slot], stream=s)
+            else:
+                self.local.export_global_device(self.ent[slot], self.cap, self.meta[slot],
+                                                self.gidx, self.gidx.numel(), rec_frame=rec_frame,
+                                                rec_frame_cap=rec_cap, stream=s)
 
     def merge(self, slot: int, out_id: torch.Tensor | None, n_dev: torch.Tensor | None,
               n_max: int, stream: int | None = None, rec_frame=None):
         """All-gather slot's tables (RCCL, current torch stream), merge them on this GPU
-        and rewrite out_id from local to global ids, on `stream`."""
-        all_ent, all_meta = gather_tables(self.ent[slot], self.meta[slot], self.group)
-        self.merged.merge_device(all_ent, self.world, self.cap, all_meta, self.max_total,
-                                 self.ids, stream=stream)
-        if self.gidx is not None:
-            # merged first_seen: global frame index -> global record index
-            mcap = self.world * self.cap
-            self.fs_counts.zero_()
-            self.merged.records_before_device(rec_frame, self.gidx, n_dev, n_max,
-                                              self.fs_counts, mcap, stream=stream)
-            dist.all_reduce(self.fs_counts, group=self.group)
-            self.merged.set_first_seen_device(self.fs_counts, mcap, stream=stream)
-        if out_id is not None:
-            lo = self.rank * self.cap
-            _parser.remap_ids_device(out_id, n_max, n_dev, self.ids[lo:lo + self.cap],
-                                     self.cap, stream=stream)
+        and rewrite out_id from local to global ids, on `stream` (rank_stream)."""
+        with rank_stream(self.merged, stream) as s:
+            all_ent, all_meta = gather_tables(self.ent[slot], self.meta[slot], self.group)
+            self.merged.merge_device(all_ent, self.world, self.cap, all_meta, self.max_total,
+                                     self.ids, stream=s)
+            if self.gidx is not None:
+                # merged first_seen: global frame index -> global record index
+                mcap = self.world * self.cap
+                self.fs_counts.zero_()
+                self.merged.records_before_device(rec_frame, self.gidx, n_dev, n_max,
+                                                  self.fs_counts, mcap, stream=s)
+                dist.all_reduce(self.fs_counts, group=self.group)
+                self.merged.set_first_seen_device(self.fs_counts, mcap, stream=s)
+            if out_id is not None:
+                lo = self.rank * self.cap
+                _parser.remap_ids_device(out_id, n_max, n_dev, self.ids[lo:lo + self.cap],
+                                         self.cap, stream=s)
         return all_ent, all_meta
 
     def step(self, out_id: torch.Tensor | None, n_dev: torch.Tensor | None, n_max: int,
              stream: int | None = None, rec_frame=None):
-        """export + merge on one stream (the torch current stream must be `stream`)."""
-        self.export(0, stream=stream, rec_frame=rec_frame, rec_cap=n_max)
-        return self.merge(0, out_id, n_dev, n_max, stream=stream, rec_frame=rec_frame)
+        """export + merge on one stream (rank_stream: torch's current one, or with
+        stream 0 / None the local context's, made current for the collectives)."""
+        with rank_stream(self.local, stream) as s:
+            self.export(0, stream=s, rec_frame=rec_frame, rec_cap=n_max)
+            return self.merge(0, out_id, n_dev, n_max, stream=s, rec_frame=rec_frame)
 
 
 class OverlappedMerge:
@@ -257,8 +288,9 @@ class FlowHashExchange:
              out_hash, out_id, out_n, counters, stream: int, filter_port: int = 0,
              direction: int = 0, rec_frame=None, ids_stream: int | None = None,
              gidx: torch.Tensor | None = None) -> None:
-        """Parse this rank's frames of the next window with global flow ids (torch's
-        current stream must be `stream`). gidx: the window's local frame -> global
+        """Parse this rank's frames of the next window with global flow ids, every call
+        and collective on one stream (rank_stream: torch's current stream, or with
+        stream 0 / None the context's own, ordered after and before the caller's). gidx: the window's local frame -> global
         frame index (default: the one given at construction). rec_frame (u32[out_cap]):
         the record -> frame map, needed when the shard holds frames the hook rejects;
         without it every frame must be accepted (checked on the device: the context's
@@ -266,26 +298,29 @@ class FlowHashExchange:
         counters, out_n) runs there, beside the next step's parse; order readers of
         those outputs after it."""
         gidx = self.gidx if gidx is None else gidx
-        self.local.parse_device(arena, arena_len, offset, caplen, ts_ns, n, out_rec, out_cap,
-                                out_hash, out_id, out_n, counters, filter_port=filter_port,
-                                direction=direction, stream=stream, out_frame=rec_frame,
-                                defer_ids=True, ids_stream=ids_stream)
-        if self.timing:  # the exchange's span on the stream: first frames .. global ids
-            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            ev0.record()
-        self.local.first_frames_device(self.first, self.cap, self.n, gidx, gidx.numel(),
-                                       rec_frame=rec_frame, rec_frame_cap=out_cap, stream=stream)
-        all_gather_flat(self.all_buf, self.buf, self.group)
-        b = self.windows & 1
-        _parser.global_ids_device(self.all_buf, self.all_buf[self.cap:], self.world, self.rank,
-                                  self.cap + 2, self.gmap, self.map_cap,
-                                  gbase_in=self.gtot[b:b + 1], gbase_out=self.gtot[1 - b:2 - b],
-                                  stream=stream, n_stride=self.cap + 2)
-        if self.timing:
-            ev1.record()
-            self.spans.append((ev0, ev1))
-        self.windows += 1
-        self.local.finish_device(self.gmap, self.map_cap, stream=stream)
+        with rank_stream(self.local, stream) as s:
+            self.local.parse_device(arena, arena_len, offset, caplen, ts_ns, n, out_rec, out_cap,
+                                    out_hash, out_id, out_n, counters, filter_port=filter_port,
+                                    direction=direction, stream=s, out_frame=rec_frame,
+                                    defer_ids=True, ids_stream=ids_stream)
+            if self.timing:  # the exchange's span on the stream: first frames .. global ids
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
+            self.local.first_frames_device(self.first, self.cap, self.n, gidx, gidx.numel(),
+                                           rec_frame=rec_frame, rec_frame_cap=out_cap, stream=s)
+            all_gather_flat(self.all_buf, self.buf, self.group)
+            b = self.windows & 1
+            _parser.global_ids_device(self.all_buf, self.all_buf[self.cap:], self.world,
+                                      self.rank, self.cap + 2, self.gmap, self.map_cap,
+                                      gbase_in=self.gtot[b:b + 1],
+                                      gbase_out=self.gtot[1 - b:2 - b], stream=s,
+                                      n_stride=self.cap + 2)
+            if self.timing:
+                ev1.record()
+                self.spans.append((ev0, ev1))
+            self.windows += 1
+            self.local.finish_device(self.gmap, self.map_cap, stream=s)
 
     def merged_flows(self, merged: "_parser.PacketParser", n_dev, n_max: int,
                      max_total_records: int, rec_frame=None):
@@ -349,8 +384,14 @@ class OwnerExchange:
     def step(self, arena, arena_len: int, offset, caplen, ts_ns, n: int, out_rec, out_cap: int,
              out_hash, out_id, out_n, counters, stream: int, filter_port: int = 0,
              direction: int = 0) -> None:
-        """Parse this rank's contiguous shard with global flow ids (torch's current
-        stream must be `stream`); the caller all-reduces the counters."""
+        """Parse this rank's contiguous shard with global flow ids (one stream for every
+        call and collective: rank_stream); the caller all-reduces the counters."""
+        with rank_stream(self.local, stream) as s:
+            self._step(arena, arena_len, offset, caplen, ts_ns, n, out_rec, out_cap, out_hash,
+                       out_id, out_n, counters, s, filter_port, direction)
+
+    def _step(self, arena, arena_len, offset, caplen, ts_ns, n, out_rec, out_cap, out_hash,
+              out_id, out_n, counters, stream, filter_port, direction) -> None:
         W, C = self.world, self.seg_cap
         self.local.parse_device(arena, arena_len, offset, caplen, ts_ns, n, out_rec, out_cap,
                                 out_hash, out_id, out_n, counters, filter_port=filter_port,

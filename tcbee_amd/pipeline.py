@@ -79,10 +79,20 @@ class Pipeline:
         decides: both modes alternate (ABBA order) `reps` times over the first
         `frames` frames and the faster median is kept — the pipe stays registered, or
         releases its registration and stages. Returns the timings and the choice
-        (also in self.output_mode). register_output() first."""
+        (also in self.output_mode). register_output() first.
+
+        Side effects: the timed runs write the first `frames` records and
+        ids of `trace` into the registered arrays (their previous contents are
+        overwritten), and the pipe's flow table is reset before each run and once
+        more at the end. A pipe that already holds flows is refused (ValueError)
+        rather than silently losing its table: calibrate before the first run, or
+        reset_flows() first."""
         import time
         if self._registered is None:
             raise ValueError("calibrate_output: register_output() first")
+        if self.parser.flow_count():
+            raise ValueError("calibrate_output: the pipe's flow table holds flows that "
+                             "the calibration would reset (calibrate first, or reset_flows())")
         rec, ids = self._registered
         m = min(frames, trace.n, len(rec))
         sub = trace.slice(0, m)

@@ -290,12 +290,15 @@ def run_gpu(rank, world, port, n, cap, result_dir, mode, n_flows=3000, filter_po
 
 
 def run_gpu_windows(rank, world, port, n, n_flows, bounds, cap, map_cap, result_dir,
-                    filter_port=0):
+                    filter_port=0, default_stream=False):
     """FlowHashExchange over a STREAM of windows: global frames [bounds[w],
     bounds[w+1]) form window w; each rank parses its flow-hash shard's frames inside
     it as one batch, keeping its flow table and id map (no reset between windows).
     Saves the concatenated records / global ids / global frame indices, the summed
-    counters and the local flow table with each flow's global id."""
+    counters and the local flow table with each flow's global id.
+    default_stream: torch's DEFAULT stream throughout (no set_stream; the step is
+    handed stream 0), the inputs of each window uploaded and the outputs read on it
+    (VERDICT r5 #1: the exchange must order its collectives itself)."""
     import torch
     import torch.distributed as dist
 
@@ -303,7 +306,8 @@ def run_gpu_windows(rank, world, port, n, n_flows, bounds, cap, map_cap, result_
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_stream(torch.cuda.Stream())
+    if not default_stream:
+        torch.cuda.set_stream(torch.cuda.Stream())
     import tcbee_amd
     from tcbee_amd import host
     from tcbee_amd.dist import FlowHashExchange
@@ -321,6 +325,7 @@ def run_gpu_windows(rank, world, port, n, n_flows, bounds, cap, map_cap, result_
     nrec = torch.zeros(1, dtype=torch.int64, device="cuda")
     ctr = torch.zeros(4, dtype=torch.int64, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
+    assert (s == 0) == default_stream
     out_rec, out_ids, out_g, tot = [], [], [], np.zeros(4, np.int64)
     with tcbee_amd.PacketParser(max_frames=max(wmax, 1), max_flows=map_cap) as p:
         fx = None

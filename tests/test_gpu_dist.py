@@ -223,13 +223,19 @@ def test_gpu_world4_flowhash_exchange_real_trace(gpu, oracle, tmp_path):
         assert int(x["ctr"][0]) == ctr["ingress"] and int(x["status"][0]) == 0
 
 
-@pytest.mark.parametrize("filter_port", [0, 5201])
-def test_gpu_world2_flowhash_exchange_windows(gpu, oracle, tmp_path, filter_port):
+@pytest.mark.parametrize("filter_port,stream", [(0, "own"), (5201, "own"), (0, "default"),
+                                                (5201, "default")])
+def test_gpu_world2_flowhash_exchange_windows(gpu, oracle, tmp_path, filter_port, stream):
     """A stream of windows through the flow-hash exchange (the tables are NOT reset
     between windows): flows keep their global ids across windows and new ones get
     the ids one parse of the whole trace gives. Ragged windows, one holding a single
     frame (so one rank parses an empty batch). Records, global ids, counters, and
-    each rank's table rows (pkts/bytes/tuple at their global ids) vs the oracle."""
+    each rank's table rows (pkts/bytes/tuple at their global ids) vs the oracle.
+    stream "default" (VERDICT r5 #1): no torch.cuda.set_stream, the step gets torch's
+    default stream (handle 0) and every window's inputs, outputs and the counter
+    all-reduce live on it — the exchange itself must put its device calls and its
+    collectives on one stream (dist.rank_stream); each window's data differs, so a
+    collective that read a buffer before its kernel wrote it would show."""
     import torch.multiprocessing as mp
 
     import dist_worker
@@ -238,7 +244,8 @@ def test_gpu_world2_flowhash_exchange_windows(gpu, oracle, tmp_path, filter_port
     n, flows, world = 150_000, 4000, 2
     bounds = [0, 3, 41_000, 41_001, 97_000, n]
     mp.spawn(dist_worker.run_gpu_windows, args=(world, free_port(), n, flows, bounds, 4096,
-                                                8192, str(tmp_path), filter_port),
+                                                8192, str(tmp_path), filter_port,
+                                                stream == "default"),
              nprocs=world, join=True)
     tr = mixed_trace(n, seed=404, n_flows=flows)
     rec, fh, fi, ctr, table = oracle.parse(tr, filter_port=filter_port)

@@ -641,6 +641,114 @@ def test_null_stream_after_default_stream_work(gpu, oracle):
     del busy
 
 
+@pytest.mark.parametrize("lib", ["legacy_init_hook", "product"])
+def test_legacy_init_race_pinned(gpu, oracle, lib, monkeypatch):
+    """round 5's intermittent all-zero flow ids, made deterministic.
+
+    Pre-fix, tcbee_ctx_create zero-filled the first-seen bitmap (and the look-back
+    status, the wide slots) with hipMemset on HIP's legacy default stream, and a
+    NULL-stream parse ran on the context's non-blocking stream without waiting for
+    that stream. A fill still queued behind a framework's default-stream work could
+    therefore land between K2's k_mark (which sets each new flow's first-frame bit)
+    and k_scan_words (which counts them): every new flow then ranks 0, and every
+    record's id is 0 while the record count stays right — the failure of
+    test_zipf_many_flows[1M] in gpurun_out/prod_t1.log. Here the interleaving is
+    pinned by host-released waits (variants-build test entry points):
+      1. a wait kernel on the legacy default stream (the "long default-stream
+         kernel"), released by host flag A;
+      2. the context is created behind it (the legacy-init hook: its fills queue
+         behind the wait, and create returns at once — hipMemset does not block);
+      3. the NULL-stream parse: with the hook K1 + k_mark run, then K2 holds its
+         stream on host flag B (tcbee_test_k2_hold);
+      4. flag A: the wait ends and the fills run (the test waits for them by an event
+         on the default stream); 5. flag B: K2 scans the zeroed bitmap.
+    The hook must give ids all 0 (count and records right); the product, through the
+    same steps 1-2-4 (no hold exists there), must be bit-exact: its fills are on the
+    context's stream before create returns, and its NULL-stream parse waits for the
+    legacy stream's queued work (ctx_stream)."""
+    import ctypes as C
+    import time as _t
+
+    import torch
+    hook = lib == "legacy_init_hook"
+    if hook:
+        monkeypatch.setenv("TCBEE_TEST_LEGACY_INIT", "1")
+    n, flows = 4_000_000, 10_000  # > 1M frames: the four-kernel K2 (k_mark ... k_assign)
+    tr = tcbee_amd.synth_trace(n, sizes="64", kind=1, n_flows=flows, seed=606)
+    rec, fh, fi, ctr, table = oracle.parse(tr)
+    d_arena = torch.from_numpy(np.concatenate([tr.arena, np.zeros(64, np.uint8)])).cuda()
+    d_off = torch.from_numpy(tr.offset.view(np.int64)).cuda()
+    d_len = torch.from_numpy(tr.caplen.view(np.int32)).cuda()
+    d_ts = torch.from_numpy(tr.ts_ns.view(np.int64)).cuda()
+    rec_d = torch.empty(n * 74 + 64, dtype=torch.uint8, device="cuda")
+    fi_d = torch.full((n,), -2, dtype=torch.int32, device="cuda")
+    n_d = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctr_d = torch.zeros(4, dtype=torch.int64, device="cuda")
+    states = torch.zeros(2, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    Lv = tcbee_amd._lib.lib(variants=True)
+    fa, fb = C.c_void_p(), C.c_void_p()
+    tcbee_amd._lib.check(Lv.tcbee_test_flag_create(C.byref(fa)), "flag")
+    tcbee_amd._lib.check(Lv.tcbee_test_flag_create(C.byref(fb)), "flag")
+    flag_a = C.c_uint64.from_address(fa.value)
+    flag_b = C.c_uint64.from_address(fb.value)
+    p = None
+    try:
+        # 1. the default-stream wait (10 s at most), queued first
+        tcbee_amd._lib.check(Lv.tcbee_test_wait_host_device(
+            fa, 1, 10_000_000, C.c_void_p(states.data_ptr()), None), "wait A")
+        # 2. the context, created behind it
+        t0 = _t.perf_counter()
+        p = tcbee_amd.PacketParser(max_frames=n, max_flows=flows + 1024, max_wide_flows=16,
+                                   variants=hook)
+        create_s = _t.perf_counter() - t0
+        if hook:
+            tcbee_amd._lib.check(Lv.tcbee_test_k2_hold(
+                p._h, fb, C.c_void_p(states.data_ptr() + 8)), "k2 hold")
+        # 3. the NULL-stream parse
+        p.parse_device(d_arena, len(tr.arena), d_off, d_len, d_ts, n, rec_d, n, None, fi_d,
+                       n_d, ctr_d, stream=None)
+        _t.sleep(0.2)  # (the hook: K1 + k_mark are done well before this)
+        # 4. release the default stream; wait until its queued work (the hook's fills)
+        #    has completed, without waiting on any other stream
+        flag_a.value = 1
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.default_stream())
+        t1 = _t.perf_counter()
+        while not ev.query():
+            assert _t.perf_counter() - t1 < 15, "the default stream did not drain"
+            _t.sleep(0.001)
+        # 5. release K2 (hook)
+        flag_b.value = 1
+        p.sync()
+        torch.cuda.synchronize()
+        st = states.cpu().tolist()
+        k = int(n_d.item())
+        ids = fi_d[:k].cpu().numpy().view(np.uint32)
+        assert st[0] == 3, f"the default-stream wait timed out ({st}): create blocked"
+        assert create_s < 5, create_s
+        assert k == len(rec) == n
+        assert np.array_equal(rec_d[:k * 74].cpu().numpy().reshape(-1, 74), rec)
+        if hook:
+            assert st[1] == 3, st
+            # the round-5 failure, reproduced: every record's flow id 0
+            assert not ids.any(), f"{int((ids != 0).sum())} non-zero ids"
+            assert len(np.unique(fi)) == flows
+        else:
+            assert np.array_equal(ids, fi)
+            assert ctr_d.cpu().numpy().tolist() == [ctr["ingress"], ctr["egress"],
+                                                     ctr["handled"], ctr["dropped"]]
+            assert np.array_equal(p.flows(), table) and p.status() == 0
+    finally:
+        flag_a.value = 1
+        flag_b.value = 1
+        torch.cuda.synchronize()
+        if p is not None:
+            p.close()
+        Lv.tcbee_test_flag_destroy(fa)
+        Lv.tcbee_test_flag_destroy(fb)
+
+
 @pytest.mark.parametrize("flows", [200_000, 1_000_000])
 def test_zipf_many_flows(gpu, oracle, flows):
     """Zipf(1.1) over many flows: a head flow holding ~12 % of the records beside a

@@ -191,6 +191,9 @@ def test_pipeline_shared_registration_and_calibration(gpu, oracle):
                       max_flows=1 << 12) as b:
             b.register_output(out, ids)  # already page-locked: borrowed
             check_same(b.run(t, out_rec=out, out_id=ids), want, b.flows())
+            with pytest.raises(ValueError, match="holds flows"):  # not silently
+                b.calibrate_output(t, frames=20_000, reps=1)
+            b.reset_flows()
             cal = b.calibrate_output(t, frames=20_000, reps=1)
             assert cal["chosen"] in ("registered", "staged") and cal["frames"] == 20_000
             assert b.output_mode == cal["chosen"]
@@ -210,6 +213,71 @@ def test_pipeline_shared_registration_and_calibration(gpu, oracle):
         out[:] = 0
         ids[:] = 0
         check_same(owner.run(t, out_rec=out, out_id=ids), want, owner.flows())
+
+
+def _hip_host_registered(arr: np.ndarray, byte: int = 0) -> bool:
+    """hipHostGetFlags on arr's byte `byte`, through the HIP runtime this process
+    loaded (torch's copy, the one libtcbee_amd.so shares)."""
+    import ctypes as C
+    path = None
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "libamdhip64" in line:
+                path = line.split()[-1]
+                break
+    assert path, "no HIP runtime mapped"
+    hip = C.CDLL(path)
+    flags = C.c_uint(0)
+    rc = hip.hipHostGetFlags(C.byref(flags), C.c_void_p(arr.ctypes.data + byte))
+    hip.hipGetLastError()
+    return rc == 0
+
+
+def test_pipeline_registration_refcounted(gpu, oracle):
+    """output registrations are process-wide and refcounted. (1) The pipe
+    that page-locked a pair is released FIRST: the pair stays page-locked while the
+    borrower holds it (its direct D2H runs keep exact outputs) and is unregistered
+    when the borrower releases it. (2) A borrower asking for more than the owner
+    locked (a larger cap over the same arrays) is refused, not sent past the pinned
+    range. (3) A caller's own hipHostRegister is borrowed and never unregistered."""
+    t = mixed_trace(40_000, seed=63, n_flows=300)
+    want = oracle.parse(t)
+    n = len(want[0])
+    out = np.zeros((n, 74), np.uint8)
+    ids = np.zeros(n, np.uint32)
+    kw = dict(device=0, chunk_frames=4096, window=64, depth=3, threads=2, max_flows=1 << 12)
+    assert not _hip_host_registered(out)
+    owner = Pipeline(**kw)
+    owner.register_output(out, ids)
+    assert _hip_host_registered(out) and _hip_host_registered(ids)
+    with Pipeline(**kw) as b:
+        b.register_output(out, ids)
+        owner.close()  # the owner goes first
+        assert _hip_host_registered(out) and _hip_host_registered(ids)
+        check_same(b.run(t, out_rec=out, out_id=ids), want, b.flows())
+    assert not _hip_host_registered(out) and not _hip_host_registered(ids)
+
+    half = n // 2
+    with Pipeline(**kw) as small, Pipeline(**kw) as big:
+        small.register_output(out[:half], ids[:half])
+        with pytest.raises(tcbee_amd.TcbeeError) as ei:
+            big.register_output(out, ids)  # covers more than the owner page-locked
+        assert ei.value.code == tcbee_amd._lib.EINVAL
+        big.register_output(out[:half // 2], ids[:half // 2])  # inside it: borrowed
+        small.register_output(None)
+        assert _hip_host_registered(out)  # big still holds it
+    assert not _hip_host_registered(out)
+
+    import torch
+    cr = torch.cuda.cudart()
+    assert int(cr.cudaHostRegister(out.ctypes.data, out.nbytes, 0)) == 0
+    try:
+        with Pipeline(**kw) as p:
+            p.register_output(out, None)  # the caller's registration: used as is
+            check_same(p.run(t, out_rec=out), want)
+        assert _hip_host_registered(out)  # and left to the caller
+    finally:
+        assert int(cr.cudaHostUnregister(out.ctypes.data)) == 0
 
 
 def test_pipeline_empty_and_tiny(gpu, oracle):

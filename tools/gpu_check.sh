@@ -1,7 +1,9 @@
 #!/bin/bash
-# Round 5: the GPU test suite on the current tree, then a same-box A/B of the
-# product K1/K3 against build/ab_<NAME> (the round-4 product) on config 3 and the
-# 125k-flow share shape. Each step under its own limit; a failure stops the script.
+# The GPU test suite on the current tree (all of it, or one file: tests-<name>), the
+# smoke, then a same-box A/B of the product K1/K3 against ab/ab_<NAME>
+# (tools/lib_ab.sh build) on config 3 and the 125k-flow share shape. Each step under
+# its own limit; a failure stops the script.
+#   bash tools/gpu_check.sh tests smoke ab
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp

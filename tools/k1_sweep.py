@@ -9,6 +9,7 @@ import itertools
 import json
 import os
 # TCBEE_* variants / ablations are dispatched by the variants build only
+os.environ.setdefault("TCBEE_AB_OPTIN", "1")
 os.environ.setdefault("TCBEE_AB_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tcbee_amd", "lib", "libtcbee_amd_variants.so"))
 import sys
 import time

@@ -1,17 +1,17 @@
 #!/bin/bash
-# Build the kernels of git revision REV (default HEAD) into build/ab_<REV>/ so a
+# Build the kernels of git revision REV (default HEAD) into ab/ab_<REV>/ so a
 # workload can be timed against them beside the working tree's build, each in its
 # own process on the same box (TCBEE_AB_LIB selects the library; tools only).
 #   tools/lib_ab.sh build [REV]        (here, on the CPU)
 #   tools/lib_ab.sh run REV -- CMD...  (on the GPU box: CMD with the old library)
-# REV "wt:NAME": the working tree as it is now, kept under build/ab_wt_NAME;
+# REV "wt:NAME": the working tree as it is now, kept under ab/ab_wt_NAME;
 # HIPEXTRA: extra compiler flags for that build (build-time experiment knobs, -D...)
 set -eu
 cd "$(dirname "$0")/.."
 case "${1:-}" in
   build)
     rev=${2:-HEAD}
-    d=build/ab_${rev//:/_}
+    d=ab/ab_${rev//:/_}
     rm -rf "$d"; mkdir -p "$d/tcbee_amd/csrc" "$d/include"
     case $rev in
       wt:*) cp tcbee_amd/csrc/*.hip tcbee_amd/csrc/*.h "$d/tcbee_amd/csrc/"
@@ -26,6 +26,6 @@ case "${1:-}" in
     echo "$d/libtcbee_amd.so" ;;
   run)
     rev=$2; shift 3
-    TCBEE_AB_LIB=build/ab_${rev//:/_}/libtcbee_amd.so "$@" ;;
+    TCBEE_AB_OPTIN=1 TCBEE_AB_LIB=ab/ab_${rev//:/_}/libtcbee_amd.so "$@" ;;
   *) echo "usage: $0 build [REV] | run REV -- CMD..." >&2; exit 2 ;;
 esac

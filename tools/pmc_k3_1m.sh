@@ -1,16 +1,22 @@
 #!/bin/bash
-# K3 mode 1 (k_count_chunk2 + k_count_bucket) on the whole 1M-flow trace
-# (--config4 --shard contig: 125M IMIX frames, 1M flows): what bounds it. Separate
+# K3 mode 1 (k_count_chunk2 + k_count_bucket): what bounds it. LEG=1M (default): the
+# whole 1M-flow trace (--config4 --shard contig: 125M IMIX frames); LEG=share: one
+# GPU's flow-hash share at N=8 (--config4 --virtual-world 8); outputs
+# gpurun_out/k3pmc_<LEG>_<pass>. Separate
 # --pmc passes (at most 8 SQ_ / 4 TCC_ counters each), each its own short run
 # under a hard limit (MI355X_MICROARCH.md: counters in their own runs).
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-args=(--steps 2 --warmup 1 --no-cpu --no-extra --sample-check ${K3ARGS:---config4 --shard contig})
+case ${LEG:-1M} in
+  share) legargs=(--config4 --virtual-world 8) ;;
+  *) legargs=(--config4 --shard contig) ;;
+esac
+args=(--steps 2 --warmup 1 --no-cpu --no-extra --sample-check "${legargs[@]}")
 pass() {  # name counters...
   local name=$1; shift
-  timeout -s KILL 300 rocprofv3 --pmc "$@" --output-format csv -d "gpurun_out/$name" -o run \
-    -- python bench.py "${args[@]}" > "gpurun_out/$name.log" 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc "$@" --output-format csv -d "gpurun_out/${name/k3pmc_/k3pmc_${LEG:-1M}_}" -o run \
+    -- python bench.py "${args[@]}" > "gpurun_out/${name/k3pmc_/k3pmc_${LEG:-1M}_}.log" 2>&1
   local rc=$?
   echo "=== $name rc=$rc" >&2
   [ $rc -eq 0 ] || exit $rc
