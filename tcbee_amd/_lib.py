@@ -218,6 +218,7 @@ _VARIANT_SIGS = {
     "tcbee_test_wait_host_device": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
                                               C.c_void_p]),
     "tcbee_test_k2_hold": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "tcbee_test_host_registered": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
 }
 
 _libs: dict = {}

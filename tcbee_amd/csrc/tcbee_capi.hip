@@ -1347,6 +1347,15 @@ int tcbee_test_wait_host_device(uint64_t* host_flag, uint64_t expect, uint64_t t
                                 state_dev, (hipStream_t)stream));
   return TCBEE_OK;
 }
+// *registered = 1 when the host byte p lies in a page-locked range (hipHostGetFlags,
+// the query tcbee_pipe_register_output makes).
+int tcbee_test_host_registered(const void* p, int* registered) {
+  if (!p || !registered) return TCBEE_EINVAL;
+  unsigned int flags = 0;
+  *registered = hipHostGetFlags(&flags, const_cast<void*>(p)) == hipSuccess;
+  (void)hipGetLastError();
+  return TCBEE_OK;
+}
 // Every later batch of `c` that ranks with the four-kernel K2 holds its stream between
 // k_mark and k_scan_words until *host_flag == 1 (NULL: off).
 int tcbee_test_k2_hold(tcbee_ctx* c, uint64_t* host_flag, uint64_t* state_dev) {

@@ -377,3 +377,48 @@ def run_replay(rank, world, port, pcap, prefix, db_path, filter_port, direction,
     with open(os.path.join(result_dir, f"rank{rank}.json"), "w") as f:
         json.dump({k: v for k, v in out.items() if k != "sink"}, f)
     dist.destroy_process_group()
+
+
+def run_shard_check(rank, world, port, n, n_flows, result_dir, corrupt):
+    """bench.validate_shard_global (the N>1 line's per-rank full check) on CPU tensors
+    over gloo: each rank's flow-hash shard of a synthetic trace, its "device" outputs
+    taken from the oracle run over the WHOLE trace (records, hashes, global ids) and
+    the merged table = the oracle's global table. corrupt: "" (all exact), "id" (one
+    global id changed on rank 1), "row" (one merged-table row's pkts changed) or
+    "record" (one record byte on rank 0)."""
+    import json
+
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    import tcbee_amd
+    from oracle_py import Oracle
+    from tcbee_amd import host
+
+    tr = tcbee_amd.synth_trace(n, sizes="imix", kind=1, n_flows=n_flows, seed=1234)
+    rec, fh, fi, _, table = Oracle().parse(tr)
+    g = np.nonzero(host.flowhash_owner(tr, world) == rank)[0].astype(np.int64)
+    sub = tr.select(g)
+    arena = torch.from_numpy(np.concatenate([sub.arena, np.zeros(64, np.uint8)]))
+    d_rec = torch.from_numpy(rec[g].reshape(-1).copy())
+    d_hash = torch.from_numpy(fh[g].view(np.int32).copy())
+    d_id = torch.from_numpy(fi[g].view(np.int32).copy())
+    merged = table.copy()
+    if corrupt == "id" and rank == 1:
+        d_id[len(g) // 2] += 1
+    if corrupt == "row":
+        merged["pkts"][len(merged) // 3] += 1
+    if corrupt == "record" and rank == 0:
+        d_rec[74 * 5 + 40] ^= 1
+    out = bench.validate_shard_global(
+        torch, dist, arena, torch.from_numpy(sub.offset.view(np.int64)),
+        torch.from_numpy(sub.caplen.view(np.int32)), torch.from_numpy(sub.ts_ns.view(np.int64)),
+        d_rec, d_hash, d_id, torch.from_numpy(g), len(g), len(g), merged, chunk=7000)
+    with open(os.path.join(result_dir, f"rank{rank}.json"), "w") as f:
+        json.dump(out, f)
+    dist.barrier()
+    dist.destroy_process_group()

@@ -48,12 +48,22 @@ def run_bench_world(world: int, args: list[str], timeout: int = 420, **env_extra
     return json.loads(lines[0])
 
 
-def check_leg(chk: dict, world: int):
+def check_leg(chk: dict, world: int, full: bool = True):
+    """full: every rank checked ALL of its shard — records, hashes,
+    global ids vs a host recomputation of the global first-seen order, its rows of
+    the merged table — not a 200k-record sample."""
     assert chk["all_ranks_bit_exact"] is True
     assert chk["ranks_checked"] == world
     assert chk["global_frames_ok"] and chk["global_pkts_ok"] and chk["global_ingress_ok"]
     assert chk["shard_imbalance"] < 1.01
-    assert chk["status"] == 0 and chk["sample_bit_exact"]
+    assert chk["status"] == 0
+    if full:
+        assert chk["full_bit_exact"] and chk["global_ids_exact"] and chk["merged_rows_exact"]
+        assert chk["records_hashes_exact"] and chk["full_records"] == chk["frames_local"]
+        assert chk["all_ranks_checked_in_full"] is True
+        assert chk["ranks_full_bit_exact"] == [True] * world
+    else:
+        assert chk["sample_bit_exact"]
 
 
 def test_bench_world2_flowhash_and_config4_leg(gpu):
@@ -63,6 +73,9 @@ def test_bench_world2_flowhash_and_config4_leg(gpu):
     assert out["dist"] == {"backend": "gloo", "world_size": 2}
     assert out["config"]["shard"] == "flowhash" and out["config"]["parallelism"] == "shard2"
     assert out["value"] > 0 and out["roofline"]["frac"] > 0
+    # the measured binary is named: the in-tree product library
+    assert out["lib_path"] == "tcbee_amd/lib/libtcbee_amd.so" and not out["ab_lib"]
+    assert len(out["lib_sha256_16"]) == 16
     chk = out["check"]
     check_leg(chk, 2)
     assert chk["flows"] == 10_000 and chk["pkts_total"] == 2 * 4_000_000
@@ -127,7 +140,7 @@ def test_bench_world1_over_rccl(gpu, shard):
     assert out["dist"] == {"backend": "nccl", "world_size": 1}
     assert out["config"]["shard"] == shard
     chk = out["check"]
-    check_leg(chk, 1)
+    check_leg(chk, 1, full=shard == "flowhash")
     assert chk["flows"] == 10_000 and chk["pkts_total"] == 4_000_000
 
 

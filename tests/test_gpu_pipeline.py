@@ -216,21 +216,14 @@ def test_pipeline_shared_registration_and_calibration(gpu, oracle):
 
 
 def _hip_host_registered(arr: np.ndarray, byte: int = 0) -> bool:
-    """hipHostGetFlags on arr's byte `byte`, through the HIP runtime this process
-    loaded (torch's copy, the one libtcbee_amd.so shares)."""
+    """hipHostGetFlags on arr's byte `byte` (a variants-build test entry point: the
+    query register_output makes, in the HIP runtime the pipes share)."""
     import ctypes as C
-    path = None
-    with open("/proc/self/maps") as f:
-        for line in f:
-            if "libamdhip64" in line:
-                path = line.split()[-1]
-                break
-    assert path, "no HIP runtime mapped"
-    hip = C.CDLL(path)
-    flags = C.c_uint(0)
-    rc = hip.hipHostGetFlags(C.byref(flags), C.c_void_p(arr.ctypes.data + byte))
-    hip.hipGetLastError()
-    return rc == 0
+    r = C.c_int(0)
+    Lv = tcbee_amd._lib.lib(variants=True)
+    tcbee_amd._lib.check(Lv.tcbee_test_host_registered(C.c_void_p(arr.ctypes.data + byte),
+                                                       C.byref(r)), "host_registered")
+    return bool(r.value)
 
 
 def test_pipeline_registration_refcounted(gpu, oracle):
