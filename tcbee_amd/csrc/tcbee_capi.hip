@@ -1347,12 +1347,12 @@ int tcbee_test_wait_host_device(uint64_t* host_flag, uint64_t expect, uint64_t t
                                 state_dev, (hipStream_t)stream));
   return TCBEE_OK;
 }
-// *registered = 1 when the host byte p lies in a page-locked range (hipHostGetFlags,
-// the query tcbee_pipe_register_output makes).
+// *registered = 1 when the host byte p lies in a page-locked range (the query
+// tcbee_pipe_register_output makes: hipPointerGetAttributes type == host).
 int tcbee_test_host_registered(const void* p, int* registered) {
   if (!p || !registered) return TCBEE_EINVAL;
-  unsigned int flags = 0;
-  *registered = hipHostGetFlags(&flags, const_cast<void*>(p)) == hipSuccess;
+  hipPointerAttribute_t at{};
+  *registered = hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost;
   (void)hipGetLastError();
   return TCBEE_OK;
 }

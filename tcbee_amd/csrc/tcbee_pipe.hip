@@ -214,6 +214,19 @@ struct HostReg {
 std::mutex g_reg_mu;
 std::vector<HostReg> g_regs;
 
+// Is host byte p page-locked (hipHostRegister'd or hipHostMalloc'd)? Measured on
+// this ROCm (round 6, ab/hostreg_probe): hipHostGetFlags fails for hipHostRegister'd
+// ranges (it knows hipHostMalloc only), while hipPointerGetAttributes reports
+// hipMemoryTypeHost for every byte of a registered range — so round 5's
+// hipHostGetFlags check never saw a registration, a second pipe registered the range
+// again (which HIP accepts), and the first hipHostUnregister released it for both.
+bool host_locked(const void* p) {
+  hipPointerAttribute_t at{};
+  const bool ok = hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost;
+  (void)hipGetLastError();
+  return ok;
+}
+
 hipError_t register_range(void* ptr, uint64_t bytes) {
   uint8_t* const b = static_cast<uint8_t*>(ptr);
   std::lock_guard<std::mutex> lk(g_reg_mu);
@@ -225,16 +238,11 @@ hipError_t register_range(void* ptr, uint64_t bytes) {
     if (b < r.base + r.bytes && r.base < b + bytes)
       return hipErrorInvalidValue;  // overlaps a registration without being inside it
   }
-  unsigned int flags = 0;
-  if (hipHostGetFlags(&flags, ptr) == hipSuccess) {
+  if (host_locked(b)) {
     // page-locked by the caller: borrow it if it reaches the last byte too
-    if (hipHostGetFlags(&flags, b + bytes - 1) != hipSuccess) {
-      (void)hipGetLastError();
-      return hipErrorInvalidValue;
-    }
+    if (!host_locked(b + bytes - 1)) return hipErrorInvalidValue;
     return hipSuccess;
   }
-  (void)hipGetLastError();  // (pageable: the query's error is expected)
   const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
   if (e == hipSuccess) g_regs.push_back({b, bytes, 1});
   return e;
