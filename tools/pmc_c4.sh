@@ -21,6 +21,7 @@ run() {  # name counters... -- bench args
 for leg in ${LEGS:-c3 c4 c4v8 v6}; do
   case $leg in
     v6) args=(--sizes imix6) ;;
+    c2) args=(--frames 1000000 --sizes 64 --flows 1) ;;
     c3) args=() ;;
     c4) args=(--config4) ;;
     c4v8) args=(--config4 --virtual-world 8) ;;

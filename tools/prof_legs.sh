@@ -18,7 +18,7 @@ for s in "$@"; do case $s in
   c3)   prof ${TAG:-r06}prof_c3 400 -- --no-extra --no-cpu ;;
   c4v8) prof ${TAG:-r06}prof_c4v8 400 -- --config4 --virtual-world 8 --steps 5 --warmup 1 --no-cpu --no-extra ;;
   c4)   prof ${TAG:-r06}prof_c4 400 -- --config4 --shard contig --steps 5 --warmup 1 --no-cpu --no-extra ;;
-  c2)   prof ${TAG:-r06}prof_c2 300 -- --config2 --no-extra --no-cpu --steps 200 --warmup 20 ;;
+  c2)   prof ${TAG:-r06}prof_c2 300 -- --frames 1000000 --sizes 64 --flows 1 --no-extra --no-cpu --steps 200 --warmup 20 ;;
   v6)   prof ${TAG:-r06}prof_v6 400 -- --sizes imix6 --no-extra --no-cpu ;;
   pmc)  LEGS="${LEGS:-c3 c4v8}" bash tools/pmc_c4.sh || exit $? ;;
 esac; done

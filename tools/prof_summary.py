@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
-"""Turn one box's rocprofv3 outputs (tools/r05_prof.sh) into committed summaries.
+"""Turn one box's rocprofv3 outputs (tools/prof_legs.sh) into committed summaries.
 
-  python tools/prof_summary.py TAG [--prefix r05prof]
+  python tools/prof_summary.py TAG [--prefix r06prof]
 
 reads only the directories of THIS run (no stale gpurun_out/ entries of older rounds):
   gpurun_out/<prefix>_c3/   kernel trace + stats of the headline command, and
   gpurun_out/<prefix>_c3.json  the bench line that same process printed
   gpurun_out/<prefix>_c4v8/ one GPU's flow-hash share of config 4 at N=8 (+ .json)
   gpurun_out/<prefix>_c4/   the whole 1M-flow config-4 trace on one GPU (+ .json)
+  gpurun_out/<prefix>_c2/, _v6/  config 2 (per-launch breakdown of its step) and the
+                            IPv6 leg (+ .json)
   gpurun_out/pmc_<leg>_{fetch,write,rdreq}/  K1 PMC passes (tools/pmc_c4.sh), legs
                             c3 / c4v8 / c4 / v6 when present and newer than the trace
 writes profiles/<TAG>_summary.md, <TAG>_kernel_stats.csv, <TAG>_bench.json,
@@ -37,7 +39,10 @@ LEGS = {"c3": ("config 3: 100M IMIX frames, 10k flows", "", "--no-extra --no-cpu
                  "--config4 --virtual-world 8 --steps 5 --warmup 1 --no-cpu --no-extra"),
         "c4": ("config 4, the whole 1M-flow trace on one GPU: 125M IMIX frames",
                "--config4", "--config4 --shard contig --steps 5 --warmup 1 --no-cpu --no-extra"),
-        "v6": ("config 3 over IPv6/TCP: 100M IMIX6 frames, 10k flows", "--sizes imix6", "")}
+        "v6": ("config 3 over IPv6/TCP: 100M IMIX6 frames, 10k flows", "--sizes imix6",
+               "--sizes imix6 --no-extra --no-cpu"),
+        "c2": ("config 2: 1M 64-B frames, 1 flow", "--frames 1000000 --sizes 64 --flows 1",
+               "--frames 1000000 --sizes 64 --flows 1 --steps 200 --warmup 20 --no-extra --no-cpu")}
 
 
 def pmc_values(path, kernel_sub):
@@ -74,10 +79,42 @@ def trace_k1(path):
     return statistics.mean(ds) if ds else None, ds
 
 
+def c2_breakdown(path, skip=20):
+    """Config 2's step launch by launch (the timed steps of a trace: warm-up skipped):
+    the average duration of each kernel of a step and the gaps between consecutive
+    launches, from start/end timestamps."""
+    rows = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                    r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].split("::")[-1])
+                   for r in csv.DictReader(open(path)) if "tcbee" in r["Kernel_Name"]))
+    steps, cur = [], []
+    for row in rows:  # a step starts at each k_prep or (fused small contexts) each k_parse
+        if row[2] in ("k_prep", "k_parse") and cur and any(x[2] == "k_parse" for x in cur):
+            steps.append(cur)
+            cur = []
+        cur.append(row)
+    if cur:
+        steps.append(cur)
+    steps = [s for s in steps if any(x[2] == "k_parse" for x in s)][skip:]
+    if not steps:
+        return []
+    shape = [x[2] for x in steps[0]]
+    steps = [s for s in steps if [x[2] for x in s] == shape]
+    out = [f"Per-launch breakdown over {len(steps)} timed steps (kernel trace timestamps):", "",
+           "| # | kernel | avg us | gap before (us) |", "|---|---|---|---|"]
+    for i, name in enumerate(shape):
+        dur = statistics.mean((s[i][1] - s[i][0]) / 1e3 for s in steps)
+        gap = statistics.mean((s[i][0] - s[i - 1][1]) / 1e3 for s in steps) if i else \
+            statistics.mean((b[0][0] - a[-1][1]) / 1e3 for a, b in zip(steps, steps[1:]))
+        out.append(f"| {i} | `{name}` | {dur:.1f} | {gap:.1f} |")
+    span = statistics.mean((b[0][0] - a[0][0]) / 1e3 for a, b in zip(steps, steps[1:]))
+    out += ["", f"Start-to-start step period {span:.1f} us."]
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--prefix", default="r05prof")
+    ap.add_argument("--prefix", default="r06prof")
     a = ap.parse_args()
     tag, pre = a.tag, a.prefix
     os.makedirs(PROF, exist_ok=True)
@@ -103,7 +140,9 @@ def main():
                   f"(frac {b['roofline']['frac']}).", "",
                   "```", line.strip(), "```", ""]
     for leg, name, title in (("c4v8", "config4_share", "config 4, one GPU's flow-hash share at N=8"),
-                             ("c4", "config4_whole", "config 4, the whole 1M-flow trace on one GPU")):
+                             ("c4", "config4_whole", "config 4, the whole 1M-flow trace on one GPU"),
+                             ("v6", "ipv6", "config 3 over IPv6/TCP (100M IMIX6 frames)"),
+                             ("c2", "config2", "config 2 (1M x 64 B, one flow): the step per launch")):
         d = os.path.join(OUT, f"{pre}_{leg}")
         if not os.path.isdir(d):
             continue
@@ -111,6 +150,8 @@ def main():
         lines += [f"## {title}", "",
                   f"Command: `rocprofv3 --kernel-trace --stats -- python bench.py {LEGS[leg][2]}`.", ""]
         lines += stats_table(os.path.join(d, "run_kernel_stats.csv")) + [""]
+        if leg == "c2":
+            lines += c2_breakdown(os.path.join(d, "run_kernel_trace.csv")) + [""]
         try:
             ln = next(x for x in open(os.path.join(OUT, f"{pre}_{leg}.json")) if x.startswith("{"))
             bl = json.loads(ln)
@@ -136,7 +177,8 @@ def main():
                 rd.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
         rd = {k: statistics.median(v) for k, v in rd.items()}
         frames = frames_of(os.path.join(OUT, f"pmc_{leg}_fetch.log"),
-                           100_000_000 if leg in ("c3", "v6") else 125_000_000)
+                           {"c3": 100_000_000, "v6": 100_000_000,
+                            "c2": 1_000_000}.get(leg, 125_000_000))
         fetch, write = fk * 1024 * 2, wk * 1024
         pmc_legs[leg] = {"workload": what, "command": "bench.py --steps 2 --warmup 1 --no-cpu "
                          f"--no-extra --sample-check {args}".strip(), "frames": frames,
