@@ -112,6 +112,7 @@ def rss_for(torch, n_global, world, kind, n_flows, seed, stream):
     skew = float(flows_per_rank.max() / max(flows_per_rank.mean(), 1e-9))
     if world >= 2 and kind == 1:
         info["flows_per_rank"] = [int(flows_per_rank.min()), int(flows_per_rank.max())]
+        info["flows_imbalance"] = round(skew, 4)  # max / mean flows per rank
         if skew > RSS_SKEW_LIMIT:
             raise RuntimeError(
                 f"flow-hash partition refused before the timed region: its busiest rank "

@@ -370,8 +370,14 @@ constexpr uint32_t kSmallNb = 512, kStagedMinNb = 64;
 // k_count_chunk2's chunk: the records one 512-thread workgroup sorts by bucket in
 // LDS at a time (24 per thread, 76 KiB: two workgroups per CU); the bucket pass sees
 // chunk q as the segment [q * kChunk, (q+1) * kChunk)
-constexpr uint32_t kChunk = 12288;
-constexpr int kChunkBlock = 512;
+#ifndef TCBEE_K3_CHUNK
+#define TCBEE_K3_CHUNK 12288
+#endif
+constexpr uint32_t kChunk = TCBEE_K3_CHUNK;
+#ifndef TCBEE_K3_CHUNK_BLOCK
+#define TCBEE_K3_CHUNK_BLOCK 512
+#endif
+constexpr int kChunkBlock = TCBEE_K3_CHUNK_BLOCK;
 // chunked mode up to kChunkMaxNb - 1 buckets: the scan of nb + 1 counts takes one
 // per thread of the smaller (512-thread) workgroup
 constexpr uint32_t kChunkMaxNb = 511;

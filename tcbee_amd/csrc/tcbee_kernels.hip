@@ -1758,6 +1758,140 @@ void k_count_chunk2(CountArgs c) {
   }
 }
 
+#if TCBEE_K3_SRT
+// Round-6 A/B (build knob TCBEE_K3_SRT): k_count_chunk2 with the chunk's WORDS placed
+// at their bucket-sorted slots (u32 s_srt[idx] = word) instead of positions (u16
+// s_pos[idx] = pos + u32 s_rw[pos] = word). Each thread keeps the sorted slot idx of
+// its 24 records in registers; the walk reads and rewrites s_srt[idx] in sorted order
+// (linear: the id replaces the word in the same slot), and the record-order store
+// reads s_srt[idx] back per record. Random LDS accesses per record: the ranking add,
+// the s_co read, the scatter, the final read — 4 instead of 5 — and 4 B of LDS per
+// record instead of 6 (48 KiB per workgroup: three workgroups per CU). Every caplen of
+// >= kLenSat goes to the flow's counter by a device atomic in phase 1 (its region
+// entry carries caplen 0), so the walk never needs the record's position.
+#ifndef TCBEE_K3_SRT_WAVES
+#define TCBEE_K3_SRT_WAVES 6  // waves per SIMD: 6 = three 512-thread workgroups per CU
+#endif
+template <bool PACK>
+__global__ __launch_bounds__(kChunkBlock) __attribute__((amdgpu_waves_per_eu(TCBEE_K3_SRT_WAVES, 8)))
+void k_count_chunk_srt(CountArgs c) {
+  constexpr int BS = kChunkBlock, U = kChunk / kChunkBlock, CH = kChunk;
+  __shared__ uint32_t s_srt[CH];
+  __shared__ uint32_t s_ch[kChunkMaxNb + 1], s_co[kChunkMaxNb + 1];
+  __shared__ uint32_t s_w[BS / 64];
+  const uint64_t nflows = c.batch->flow_total;
+  if (count_mode(c, nflows) != 1 || !chunk_scatter(c, nflows)) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);
+  uint32_t sh = 8;
+  while (sh < kBucketBits && ((nflows + (1ull << sh) - 1) >> sh) >= kChunkMaxNb) ++sh;
+  const uint32_t nsb = (uint32_t)((nflows + (1ull << sh) - 1) >> sh);
+  const uint32_t rsh = kBucketBits - sh;
+  const uint64_t n_acc = c.batch->n_acc;
+  const uint64_t nchunks = (n_acc + CH - 1) / CH;
+  const uint32_t lmax = 0xFFFFFFFFu >> c.pack_bits;
+  for (uint32_t b = tid; b <= nsb; b += BS) s_ch[b] = 0;
+  __syncthreads();
+  for (uint64_t q = blockIdx.x; q < nchunks; q += gridDim.x) {
+    const uint64_t base = q * CH;
+    const uint64_t hi = base + CH < n_acc ? base + CH : n_acc;
+    const uint32_t nval = (uint32_t)(hi - base);
+    uint32_t w[U], lp[U];
+    const uint32_t* af = c.acc_flow + base;
+    const uint32_t* al = c.acc_len + base;
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint32_t pos = (uint32_t)k * BS + tid;
+      w[k] = __builtin_nontemporal_load(&af[pos < nval ? pos : 0u]);
+      if (!PACK) lp[k] = __builtin_nontemporal_load(&al[pos < nval ? pos : 0u]);
+    }
+    bool rare = false;
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint32_t pos = (uint32_t)k * BS + tid;
+      const uint32_t v = w[k];
+      uint32_t cl = PACK ? (v == 0xFFFFFFFFu ? v : (v & ((1u << c.pack_bits) - 1u))) : v;
+      const uint32_t len = PACK ? (v >> c.pack_bits) : lp[k];
+      if (pos >= nval) cl = 0xFFFFFFFFu;
+      rare |= cl != 0xFFFFFFFFu && len >= kLenSat;
+      w[k] = cl == 0xFFFFFFFFu ? 0xFFFFFFFFu : (cl | (len < kLenSat ? len : kLenSat) << 21);
+    }
+    if (__any(rare)) {  // caplens of >= kLenSat: their bytes by a device atomic, field 0
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint32_t pos = (uint32_t)k * BS + tid;
+        const uint32_t cl = w[k] == 0xFFFFFFFFu ? w[k] : (w[k] & 0x1FFFFFu);
+        if (cl == 0xFFFFFFFFu || (w[k] >> 21) != kLenSat) continue;
+        uint32_t len = PACK ? (af[pos] >> c.pack_bits) : al[pos];
+        if (PACK && len == lmax) len = al[pos];
+        if ((cl >> kBucketBits) < nb)
+          atomicAdd((unsigned long long*)&c.cnt[2ull * c.cmap[cl] + 1], (unsigned long long)len);
+        w[k] = cl;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const bool valid = (uint32_t)k * BS + tid < nval;
+      const uint32_t bk = w[k] == 0xFFFFFFFFu ? nsb : (w[k] & 0x1FFFFFu) >> sh;
+      const uint32_t b0 = __builtin_amdgcn_readfirstlane(bk);
+      const uint64_t vm = __ballot(valid);
+      if (__all(!valid || bk == b0)) {
+        uint32_t r0 = 0;
+        if (lane == 0 && vm) r0 = atomicAdd(&s_ch[b0], (uint32_t)__popcll(vm));
+        r0 = __shfl(r0, 0);
+        lp[k] = r0 + (uint32_t)__popcll(vm & lanemask_lt());
+      } else {
+        lp[k] = valid ? atomicAdd(&s_ch[bk], 1u) : 0u;
+      }
+    }
+    __syncthreads();
+    {
+      uint32_t tot;
+      const uint32_t off = block1024_excl_scan<BS>(tid <= nsb ? s_ch[tid] : 0u, s_w, tot);
+      if (tid <= nsb) s_co[tid] = off;
+      if (tid <= nsb) s_ch[tid] = 0;
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j <= nb; j += BS)
+      c.coffs[q * (kChunkMaxNb + 1) + j] = s_co[j < nb ? j << rsh : nsb];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint32_t pos = (uint32_t)k * BS + tid;
+      if (pos >= nval) continue;
+      const uint32_t bk = w[k] == 0xFFFFFFFFu ? nsb : (w[k] & 0x1FFFFFu) >> sh;
+      lp[k] += s_co[bk];  // the record's sorted slot
+      s_srt[lp[k]] = w[k];
+    }
+    __syncthreads();
+    uint32_t* rg = c.region + base;
+#pragma unroll 6
+    for (int k = 0; k < U; ++k) {
+      const uint32_t idx = (uint32_t)k * BS + tid;
+      if (idx >= nval) continue;
+      const uint32_t x = s_srt[idx];
+      uint32_t id = 0xFFFFFFFFu;
+      const uint32_t cl = x & 0x1FFFFFu;
+      if (x != 0xFFFFFFFFu && (cl >> kBucketBits) < nb) {
+        rg[idx] = (cl & (kBucket - 1u)) | (x >> 21) << kBucketBits;
+        id = c.omap[cl];
+      }
+      s_srt[idx] = id;  // the slot this thread just read
+    }
+    __syncthreads();
+    if (c.out_id && base < c.out_cap) {
+      uint32_t* oi = c.out_id + base;
+      const uint32_t lim = c.out_cap - base < nval ? (uint32_t)(c.out_cap - base) : nval;
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint32_t pos = (uint32_t)k * BS + tid;
+        if (pos < lim) __builtin_nontemporal_store(s_srt[lp[k]], &oi[pos]);
+      }
+    }
+    __syncthreads();  // (s_srt is rewritten by the next chunk's scatter)
+  }
+}
+#endif
+
 // Mode 1, phase 2: workgroup (j, s) histograms bucket j over the segments of K3
 // blocks s, s+S, ... (S = gridDim / nb) in LDS; each wave walks one block's
 // segment at a time, 4 records per lane in flight. Writes a dense partial row.
@@ -2137,9 +2271,19 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
   if (g2) {
     if (c.coffs) {
       // kChunk-record chunks in 76 KiB of LDS: two 512-thread workgroups per CU
+#if TCBEE_K3_SRT
+      // (48 KiB of LDS: three workgroups per CU)
+#ifndef TCBEE_K3_SRT_WGS
+#define TCBEE_K3_SRT_WGS 2  // resident workgroups per CU
+#endif
+      const dim3 gc(g1s ? (g1s * TCBEE_K3_SRT_WGS + 1) / 2 : 1);
+      if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk_srt<true>), gc, dim3(kChunkBlock), 0, s, c);
+      else hipLaunchKernelGGL((k_count_chunk_srt<false>), gc, dim3(kChunkBlock), 0, s, c);
+#else
       const dim3 gc(g1s ? g1s : 1);
       if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk2<true>), gc, dim3(kChunkBlock), 0, s, c);
       else hipLaunchKernelGGL((k_count_chunk2<false>), gc, dim3(kChunkBlock), 0, s, c);
+#endif
     }
     hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1s);
   }
