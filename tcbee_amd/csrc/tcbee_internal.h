@@ -368,8 +368,9 @@ constexpr uint32_t kMaxBuckets = 4096;    // mode 1 up to 16M flows (hist + curs
 // bucket cursors and the per-chunk barriers cost more than they save
 constexpr uint32_t kSmallNb = 512, kStagedMinNb = 64;
 // k_count_chunk2's chunk: the records one 512-thread workgroup sorts by bucket in
-// LDS at a time (24 per thread, 76 KiB: two workgroups per CU); the bucket pass sees
-// chunk q as the segment [q * kChunk, (q+1) * kChunk)
+// LDS at a time (24 per thread, 52 KiB: two workgroups per CU); the bucket pass sees
+// chunk q as the segment [q * kChunk, (q+1) * kChunk). TCBEE_K3_CHUNK /
+// TCBEE_K3_CHUNK_BLOCK: build-time A/B knobs (round 6: 16384 and 1024 x 24576 slower)
 #ifndef TCBEE_K3_CHUNK
 #define TCBEE_K3_CHUNK 12288
 #endif

@@ -1584,197 +1584,39 @@ __global__ __launch_bounds__(kCountBlock) void k_count_scatter_staged(CountArgs 
 
 // Mode 1, single pass (nb < kChunkMaxNb): each 512-thread workgroup takes chunks of
 // kChunk = 12288 accepted records (24 per thread) and
-//  1. ranks them by bucket in LDS (counts per bucket, one LDS add per record or one
-//     per wave when the wave's records share a bucket; no-flow records go to a
-//     spare bucket nb), scans the counts;
-//  2. places every record's chunk position at its bucket-sorted slot in LDS;
-//  3. walks the sorted entries with consecutive lanes on consecutive entries: the
+//  1. ranks them by sub-bin in LDS (counts per sub-bin, one LDS add per record or one
+//     per wave when the wave's records share a sub-bin; no-flow records go to a spare
+//     sub-bin nsb), scans the counts;
+//  2. places every record's WORD at its sorted slot (s_srt[idx] = claim | caplen),
+//     the thread keeping each of its records' slot idx in a register;
+//  3. walks the sorted slots with consecutive lanes on consecutive entries: the
 //     region entry (claim within the bucket | caplen) is stored coalesced at
 //     region[chunk + idx] (the chunk's buckets are contiguous runs; coffs[q] = their
-//     offsets for k_count_bucket) and the claim -> output id gather reads omap inside
-//     one bucket's 16 KiB window per wave, where a record-order gather hits random
-//     lines of a table of every flow;
-//  4. writes each id back to its record position in LDS and stores the chunk's ids
-//     in record order, coalesced.
+//     offsets for k_count_bucket), the claim -> output id gather reads omap inside a
+//     few sub-bins' windows per wave (a record-order gather hits a random line of the
+//     whole map per lane: 692 us per 125M records at 125k flows, tools/
+//     k3_gather_floor.hip), and the id replaces the word in the slot just read;
+//  4. stores the chunk's ids in record order, coalesced: each thread reads its
+//     records' slots back.
 // One pass over the K1 -> K3 words, no per-block cursors, no scattered stores.
-// 76 KiB of LDS, so TWO workgroups share a CU and one's barrier waits hide under the
-// other's loads and gathers (round 3; round 2's 16384-record form needed 132 KiB and
-// ran latency-bound at 2.5 TB/s, one workgroup per CU; 1024 x 12 and three 8192-record
-// workgroups per CU were slower too). Per chunk:
-//  s_rw[pos]  = claim | min(caplen, kLenSat) << 21 of the record at chunk position
-//               pos (claims < 510 * 4096 < 2^21 wherever the chunked mode runs;
-//               ~0 = no flow); after the gather, the record's output id
-//  s_pos[idx] = the chunk position of bucket-sorted entry idx (u16)
-// 6 B per record. The sorted walk reads s_pos[idx] -> s_rw[pos], stores the region
-// entry at region[chunk + idx] and the id back into s_rw[pos] — a slot only its own
-// reader touches, so no barrier between the gather and the write-back.
-constexpr uint32_t kLenSat = 2047;  // caplens >= kLenSat are re-read from the K1 scratch
+// Round 6: the words themselves at their sorted slots — round 3-5 sorted u16
+// positions (s_pos[idx] = pos) beside a record-order word array (s_rw[pos]), one more
+// random LDS access per record (five: the ranking add, the s_co read, the position
+// scatter, the walk's s_rw[pos] read and write-back; now four) and 6 B of LDS per
+// record instead of 4; its scratch spill (24 B/lane) is gone too. Per 100M records,
+// same box, alternating processes (profiles/r06_k3_ab.log): 125k flows 322.5 -> 296.5
+// us, 1M flows 498.4 -> 480.9 us. Refuted in the same A/B: three workgroups per CU
+// (6 waves/SIMD: 96 B/lane of spills, 366 / 633 us), 16384-record chunks (spills,
+// 354 / 504) and 1024-thread workgroups of 24576 records (335 / 530; their longer
+// bucket runs took k_count_bucket at 1M flows 156 -> 125 us, not enough).
+// Every caplen of >= kLenSat (2047 B: never on an IMIX trace) goes to the flow's
+// counter by a device atomic in phase 1 and its region entry carries caplen 0, so the
+// walk never needs the record's position (round 5 re-read it there).
+// 52 KiB of LDS and 128 VGPRs: two workgroups per CU (4 waves / SIMD).
+constexpr uint32_t kLenSat = 2047;  // caplens >= kLenSat: bytes by a device atomic
 template <bool PACK>
 __global__ __launch_bounds__(kChunkBlock) __attribute__((amdgpu_waves_per_eu(2 * kChunkBlock / 256, 8)))
 void k_count_chunk2(CountArgs c) {
-  constexpr int BS = kChunkBlock, U = kChunk / kChunkBlock, CH = kChunk;
-  __shared__ uint32_t s_rw[CH];
-  __shared__ uint16_t s_pos[CH];
-  __shared__ uint32_t s_ch[kChunkMaxNb + 1], s_co[kChunkMaxNb + 1];
-  __shared__ uint32_t s_w[BS / 64];
-  static_assert(CH <= (1 << 16) && kChunkMaxNb < BS && (uint64_t)kChunkMaxNb * kBucket < (1u << 21),
-                "layout");
-  const uint64_t nflows = c.batch->flow_total;
-  if (count_mode(c, nflows) != 1 || !chunk_scatter(c, nflows)) return;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t nb = (uint32_t)((nflows + kBucket - 1) >> kBucketBits);
-  // The chunk is sorted by SUB-BIN = claim >> sh, the finest key whose bins fit the
-  // LDS counters (<= kChunkMaxNb - 1 of them): a refinement of the bucket order
-  // (claim >> kBucketBits), so each bucket is still one contiguous run of the chunk,
-  // but neighbouring lanes of the sorted walk gather claim -> id from fewer lines
-  // (125k flows: bins of 256 claims = 1 KiB of omap instead of 16 KiB; 1M flows:
-  // 2048 claims) and the ranking's adds spread over more LDS addresses.
-  uint32_t sh = 8;
-  while (sh < kBucketBits && ((nflows + (1ull << sh) - 1) >> sh) >= kChunkMaxNb) ++sh;
-  const uint32_t nsb = (uint32_t)((nflows + (1ull << sh) - 1) >> sh);  // spare sub-bin: nsb
-  const uint32_t rsh = kBucketBits - sh;  // bucket j starts at sub-bin j << rsh
-  const uint64_t n_acc = c.batch->n_acc;
-  const uint64_t nchunks = (n_acc + CH - 1) / CH;
-  const uint32_t lmax = 0xFFFFFFFFu >> c.pack_bits;
-  for (uint32_t b = tid; b <= nsb; b += BS) s_ch[b] = 0;
-  __syncthreads();
-  for (uint64_t q = blockIdx.x; q < nchunks; q += gridDim.x) {
-    const uint64_t base = q * CH;
-    const uint64_t hi = base + CH < n_acc ? base + CH : n_acc;
-    const uint32_t nval = (uint32_t)(hi - base);
-    uint32_t w[U], lp[U];
-    // chunk-relative 32-bit offsets from a uniform base: global loads with an SGPR
-    // base address (64-bit per-lane addresses cost the registers that let two
-    // workgroups share a CU)
-    const uint32_t* af = c.acc_flow + base;
-    const uint32_t* al = c.acc_len + base;
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const uint32_t pos = (uint32_t)k * BS + tid;
-      w[k] = __builtin_nontemporal_load(&af[pos < nval ? pos : 0u]);
-      if (!PACK) lp[k] = __builtin_nontemporal_load(&al[pos < nval ? pos : 0u]);  // (lp: len)
-    }
-    // decode: claim | min(caplen, kLenSat) << 21 (~0: no flow). A caplen of
-    // >= kLenSat (2047 B: never on an IMIX trace) is rare: the wave then redoes its
-    // words with the full value (the side array when the packed field saturated) and
-    // sends a caplen past the region field to the flow's counter by a device atomic;
-    // the common path has no per-word branches (their exec masks cost registers)
-    bool rare = false;
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const uint32_t pos = (uint32_t)k * BS + tid;
-      const uint32_t v = w[k];
-      uint32_t cl = PACK ? (v == 0xFFFFFFFFu ? v : (v & ((1u << c.pack_bits) - 1u))) : v;
-      const uint32_t len = PACK ? (v >> c.pack_bits) : lp[k];
-      if (pos >= nval) cl = 0xFFFFFFFFu;
-      rare |= cl != 0xFFFFFFFFu && len >= kLenSat;
-      w[k] = cl == 0xFFFFFFFFu ? 0xFFFFFFFFu : (cl | (len < kLenSat ? len : kLenSat) << 21);
-    }
-    if (__any(rare)) {
-#pragma unroll
-      for (int k = 0; k < U; ++k) {
-        const uint32_t pos = (uint32_t)k * BS + tid;
-        const uint32_t cl = w[k] == 0xFFFFFFFFu ? w[k] : (w[k] & 0x1FFFFFu);
-        if (cl == 0xFFFFFFFFu || (w[k] >> 21) != kLenSat) continue;
-        uint32_t len = PACK ? (af[pos] >> c.pack_bits) : al[pos];
-        if (PACK && len == lmax) len = al[pos];  // saturated packed field: the side array
-        if (len >= kRegLenEsc) {  // past the region entry's field: counted here
-          atomicAdd((unsigned long long*)&c.cnt[2ull * c.cmap[cl] + 1], (unsigned long long)len);
-          w[k] = cl;  // caplen 0 in the region entry
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const bool valid = (uint32_t)k * BS + tid < nval;
-      const uint32_t bk = w[k] == 0xFFFFFFFFu ? nsb : (w[k] & 0x1FFFFFu) >> sh;
-      const uint32_t b0 = __builtin_amdgcn_readfirstlane(bk);
-      const uint64_t vm = __ballot(valid);
-      if (__all(!valid || bk == b0)) {
-        // one add for the wave (a hot flow's bucket): ranks in lane order
-        uint32_t r0 = 0;
-        if (lane == 0 && vm) r0 = atomicAdd(&s_ch[b0], (uint32_t)__popcll(vm));
-        r0 = __shfl(r0, 0);
-        lp[k] = r0 + (uint32_t)__popcll(vm & lanemask_lt());
-      } else {
-        lp[k] = valid ? atomicAdd(&s_ch[bk], 1u) : 0u;
-      }
-    }
-    __syncthreads();
-    {
-      uint32_t tot;
-      const uint32_t off = block1024_excl_scan<BS>(tid <= nsb ? s_ch[tid] : 0u, s_w, tot);
-      if (tid <= nsb) s_co[tid] = off;
-      if (tid <= nsb) s_ch[tid] = 0;  // read by the scan only: zero for the next chunk
-    }
-    __syncthreads();
-    // the bucket pass's offsets: bucket j = sub-bins [j << rsh, (j + 1) << rsh); [nb] =
-    // the end of the real buckets (the spare sub-bin's start)
-    for (uint32_t j = tid; j <= nb; j += BS)
-      c.coffs[q * (kChunkMaxNb + 1) + j] = s_co[j < nb ? j << rsh : nsb];
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const uint32_t pos = (uint32_t)k * BS + tid;
-      if (pos >= nval) continue;
-      const uint32_t bk = w[k] == 0xFFFFFFFFu ? nsb : (w[k] & 0x1FFFFFu) >> sh;
-      s_pos[s_co[bk] + lp[k]] = (uint16_t)pos;
-      s_rw[pos] = w[k];
-    }
-    __syncthreads();
-    uint32_t* rg = c.region + base;
-#pragma unroll 6
-    for (int k = 0; k < U; ++k) {
-      const uint32_t idx = (uint32_t)k * BS + tid;
-      if (idx >= nval) continue;
-      const uint32_t pos = s_pos[idx];
-      const uint32_t x = s_rw[pos];
-      uint32_t id = 0xFFFFFFFFu;
-      const uint32_t cl = x & 0x1FFFFFu;
-      if (x != 0xFFFFFFFFu && (cl >> kBucketBits) < nb) {
-        uint32_t l = x >> 21;
-        if (l == kLenSat) {  // a caplen of >= 2047 B: the full value from the K1 scratch
-          if (PACK) {
-            l = af[pos] >> c.pack_bits;
-            if (l == lmax) l = al[pos];
-          } else {
-            l = al[pos];
-          }
-        }
-        rg[idx] = (cl & (kBucket - 1u)) | l << kBucketBits;  // coalesced runs
-        id = c.omap[cl];  // a few sub-bins' windows per wave: few lines
-      }
-      s_rw[pos] = id;  // only this thread reads or writes slot pos in this phase
-    }
-    __syncthreads();
-    if (c.out_id && base < c.out_cap) {
-      uint32_t* oi = c.out_id + base;
-      const uint32_t lim = c.out_cap - base < nval ? (uint32_t)(c.out_cap - base) : nval;
-#pragma unroll
-      for (int k = 0; k < U; ++k) {
-        const uint32_t pos = (uint32_t)k * BS + tid;
-        if (pos < lim) __builtin_nontemporal_store(s_rw[pos], &oi[pos]);
-      }
-    }
-  }
-}
-
-#if TCBEE_K3_SRT
-// Round-6 A/B (build knob TCBEE_K3_SRT): k_count_chunk2 with the chunk's WORDS placed
-// at their bucket-sorted slots (u32 s_srt[idx] = word) instead of positions (u16
-// s_pos[idx] = pos + u32 s_rw[pos] = word). Each thread keeps the sorted slot idx of
-// its 24 records in registers; the walk reads and rewrites s_srt[idx] in sorted order
-// (linear: the id replaces the word in the same slot), and the record-order store
-// reads s_srt[idx] back per record. Random LDS accesses per record: the ranking add,
-// the s_co read, the scatter, the final read — 4 instead of 5 — and 4 B of LDS per
-// record instead of 6 (48 KiB per workgroup: three workgroups per CU). Every caplen of
-// >= kLenSat goes to the flow's counter by a device atomic in phase 1 (its region
-// entry carries caplen 0), so the walk never needs the record's position.
-#ifndef TCBEE_K3_SRT_WAVES
-#define TCBEE_K3_SRT_WAVES 6  // waves per SIMD: 6 = three 512-thread workgroups per CU
-#endif
-template <bool PACK>
-__global__ __launch_bounds__(kChunkBlock) __attribute__((amdgpu_waves_per_eu(TCBEE_K3_SRT_WAVES, 8)))
-void k_count_chunk_srt(CountArgs c) {
   constexpr int BS = kChunkBlock, U = kChunk / kChunkBlock, CH = kChunk;
   __shared__ uint32_t s_srt[CH];
   __shared__ uint32_t s_ch[kChunkMaxNb + 1], s_co[kChunkMaxNb + 1];
@@ -1890,7 +1732,6 @@ void k_count_chunk_srt(CountArgs c) {
     __syncthreads();  // (s_srt is rewritten by the next chunk's scatter)
   }
 }
-#endif
 
 // Mode 1, phase 2: workgroup (j, s) histograms bucket j over the segments of K3
 // blocks s, s+S, ... (S = gridDim / nb) in LDS; each wave walks one block's
@@ -2270,20 +2111,10 @@ hipError_t launch_count(const CountArgs& c, unsigned g1, unsigned g1s, unsigned 
   }
   if (g2) {
     if (c.coffs) {
-      // kChunk-record chunks in 76 KiB of LDS: two 512-thread workgroups per CU
-#if TCBEE_K3_SRT
-      // (48 KiB of LDS: three workgroups per CU)
-#ifndef TCBEE_K3_SRT_WGS
-#define TCBEE_K3_SRT_WGS 2  // resident workgroups per CU
-#endif
-      const dim3 gc(g1s ? (g1s * TCBEE_K3_SRT_WGS + 1) / 2 : 1);
-      if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk_srt<true>), gc, dim3(kChunkBlock), 0, s, c);
-      else hipLaunchKernelGGL((k_count_chunk_srt<false>), gc, dim3(kChunkBlock), 0, s, c);
-#else
+      // kChunk-record chunks in 52 KiB of LDS: two 512-thread workgroups per CU
       const dim3 gc(g1s ? g1s : 1);
       if (c.pack_bits) hipLaunchKernelGGL((k_count_chunk2<true>), gc, dim3(kChunkBlock), 0, s, c);
       else hipLaunchKernelGGL((k_count_chunk2<false>), gc, dim3(kChunkBlock), 0, s, c);
-#endif
     }
     hipLaunchKernelGGL(k_count_bucket, dim3(g2), dim3(kCountBlock), 0, s, c, g1s);
   }
