@@ -414,6 +414,9 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_rec[SREC_DW];
   __shared__ uint32_t s_wcnt[FPL][NW];
   __shared__ uint64_t s_excl;
+  // per wave and frame group: the slot and record index its all-one-slot group would
+  // compete with for first_seen (~0: none), merged per tile at the end
+  __shared__ uint32_t s_fsl[NW * FPL], s_fsp[NW * FPL];
 
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint64_t tile = blockIdx.x;
@@ -689,6 +692,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
       // first_seen competition: only flows new in this batch (claim >= fbase)
       const bool mine = acc[f] && slot[f] != 0xFFFFFFFFu && claim[f] >= fbase;
       const uint64_t am = __ballot(mine);
+      if (lane == 0) s_fsp[wave * FPL + f] = 0xFFFFFFFFu;
       if (am) {
         const uint32_t leader = (uint32_t)__ffsll((unsigned long long)am) - 1;
         const uint32_t s0 = __shfl(slot[f], leader);
@@ -700,11 +704,43 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
           // competes for both (a hot new flow: one add per wave, not per group)
           const bool first = s0 != prev_s0;
           prev_s0 = s0;
-          if (first && lane == leader && fs_needs_min(fs_seen[f], frame_i, p32))
-            atomicMin(slot_fs_any(a.tab, s0), p32);
+          if (first && lane == leader && fs_needs_min(fs_seen[f], frame_i, p32)) {
+            s_fsl[wave * FPL + f] = s0;
+            s_fsp[wave * FPL + f] = p32;
+          }
         } else if (mine && fs_needs_min(fs_seen[f], frame_i, p32)) {
           atomicMin(slot_fs_any(a.tab, slot[f]), p32);
         }
+      }
+    }
+  }
+  if (FLOWS) {
+    // One competitor per slot and tile: the tile's smallest candidate, and only when
+    // the word, re-read, is still larger. A hot flow new in the batch (config 2's one
+    // flow, a Zipf head) otherwise sent one same-address device atomic per wave
+    // whose frames precede the claimer's — ~2000 of them when a late wave of the first
+    // dispatch round won the insert, serialized at the coherence point (round 6,
+    // profiles/r06_config2_attempts.log: config 2's K1 mean 50.5-56.2 -> 44.1-44.6 us,
+    // p90 63-90 -> 46-47 us, max 112-119 -> 50-51 us; with a warm table, no inserts
+    // and no competition, it is 38.3 us).
+    __syncthreads();
+    if (tid < NW * FPL) {
+      const uint32_t p0 = s_fsp[tid];
+      if (p0 != 0xFFFFFFFFu) {
+        const uint32_t sl0 = s_fsl[tid];
+        uint32_t best = p0;
+        bool owner = true;
+#pragma unroll
+        for (int e = 0; e < NW * FPL; ++e) {
+          const uint32_t pe = s_fsp[e];
+          if (pe == 0xFFFFFFFFu || s_fsl[e] != sl0 || e == (int)tid) continue;
+          if (e < (int)tid) owner = false;
+          best = pe < best ? pe : best;
+        }
+        // (an earlier tile has often lowered the word by now: a stale read is only
+        //  ever larger, so the atomic is at worst redundant)
+        if (owner && ld_agent32(slot_fs_any(a.tab, sl0)) > best)
+          atomicMin(slot_fs_any(a.tab, sl0), best);
       }
     }
   }
