@@ -449,9 +449,12 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
     for (int j = 0; j < 5; ++j) K[f][j] = 0;
     const bool in = i < a.n;
     const uint64_t ic = in ? i : a.n - 1;  // loads stay unconditional (no branch per frame)
-    const uint64_t o = a.offset[ic];
-    const uint32_t l = a.caplen[ic];
-    tsv[f] = a.ts[ic];
+    // the streamed-once index with the non-temporal hint (round 6: config 3 K1 -1.0 %,
+    // the share -0.4 %, profiles/r06_idx_nt_ab.log; the header windows keep the
+    // default policy — nt there filled the same lines and was 20 % slower, round 2)
+    const uint64_t o = __builtin_nontemporal_load(&a.offset[ic]);
+    const uint32_t l = __builtin_nontemporal_load(&a.caplen[ic]);
+    tsv[f] = __builtin_nontemporal_load(&a.ts[ic]);
     offv[f] = in ? o : 0;
     clen[f] = in ? l : 0;
   }
