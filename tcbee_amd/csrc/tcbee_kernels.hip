@@ -390,7 +390,11 @@ __device__ __forceinline__ void copy_out(uint8_t* __restrict__ out, uint64_t G0,
       }
       u32x4 ov;
       ov[0] = o.x; ov[1] = o.y; ov[2] = o.z; ov[3] = o.w;
-      *reinterpret_cast<u32x4*>(out + g) = ov;
+      // non-temporal (round 6: the records are written once and read by the host or
+      // the next stage, never by this kernel; config 3 K1 -3.8 %, the share -1.7 %,
+      // profiles/r06_store_nt_ab.log — round 1's non-temporal record stores, issued
+      // lane by lane before the LDS staging existed, were slower)
+      __builtin_nontemporal_store(ov, reinterpret_cast<u32x4*>(out + g));
     } else {
       const uint64_t lo = g > G0 ? g : G0;
       const uint64_t hi = (g + 16) < G1 ? (g + 16) : G1;
@@ -674,7 +678,8 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   for (int f = 0; f < FPL; ++f) {
     const uint64_t p = excl + rank[f];
     if (acc[f]) {
-      if (a.out_hash && p < a.out_cap) a.out_hash[p] = hsh[f];
+      // (side words non-temporal too: -0.35 % on config 3's K1, round 6)
+      if (a.out_hash && p < a.out_cap) __builtin_nontemporal_store(hsh[f], &a.out_hash[p]);
       // record -> frame map (flow-hash shards of traces with rejected frames)
       if (a.out_frame && p < a.out_cap) a.out_frame[p] = (uint32_t)(i0 + (uint64_t)f * kBlock + tid);
       if (FLOWS) {
@@ -683,7 +688,8 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
           // field and is stored in full beside it (K3 reads it only then)
           const uint32_t lmax = 0xFFFFFFFFu >> a.pack_bits;
           const uint32_t lq = clen[f] < lmax ? clen[f] : lmax;
-          a.acc_flow[p] = claim[f] == 0xFFFFFFFFu ? 0xFFFFFFFFu : claim[f] | (lq << a.pack_bits);
+          __builtin_nontemporal_store(claim[f] == 0xFFFFFFFFu ? 0xFFFFFFFFu : claim[f] | (lq << a.pack_bits),
+                                      &a.acc_flow[p]);
           if (lq == lmax) a.acc_len[p] = clen[f];
         } else {
           a.acc_flow[p] = claim[f];
