@@ -663,7 +663,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   if (tid == 0 && tile == a.ntiles - 1) a.batch->n_acc = excl + total;
 
   // ---- records: LDS -> HBM, 16-B stores, partial chunks as 2-B stores ----
-  // (non-temporal record stores were slower, round 1)
+  // (non-temporal 16-B stores, see copy_out)
   {
     const uint64_t wr_lo = excl < a.out_cap ? excl : a.out_cap;
     const uint64_t wr_hi = (excl + total) < a.out_cap ? (excl + total) : a.out_cap;
