@@ -641,6 +641,40 @@ def test_null_stream_after_default_stream_work(gpu, oracle):
     del busy
 
 
+def test_null_stream_parse_with_another_device_current(gpu, oracle):
+    """a NULL-stream call records the legacy default stream of the CURRENT
+    device; ctx_stream now makes the context's device current first, so a thread whose
+    current device is another GPU still orders the parse after the right device's
+    default-stream work. Needs two GPUs (skipped on a one-GPU box)."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two HIP devices")
+    tr = tcbee_amd.synth_trace(300_000, sizes="imix", kind=1, n_flows=5000, seed=88)
+    rec, fh, fi, ctr, table = oracle.parse(tr)
+    n = tr.n
+    with torch.cuda.device(1):
+        d_arena = torch.from_numpy(np.concatenate([tr.arena, np.zeros(64, np.uint8)])).cuda()
+        d_off = torch.from_numpy(tr.offset.view(np.int64)).cuda()
+        d_len = torch.from_numpy(tr.caplen.view(np.int32)).cuda()
+        d_ts = torch.from_numpy(tr.ts_ns.view(np.int64)).cuda()
+        rec_d = torch.full((n * 74 + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+        fi_d = torch.full((n,), -2, dtype=torch.int32, device="cuda")
+        n_d = torch.zeros(1, dtype=torch.int64, device="cuda")
+        ctr_d = torch.zeros(4, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize(1)
+    with tcbee_amd.PacketParser(device=1, max_frames=n, max_flows=8192) as p:
+        torch.cuda.set_device(0)
+        p.parse_device(d_arena, len(tr.arena), d_off, d_len, d_ts, n, rec_d, n, None, fi_d, n_d,
+                       ctr_d, stream=None)
+        p.sync()
+        torch.cuda.synchronize(1)
+        k = int(n_d.item())
+        assert k == len(rec)
+        assert np.array_equal(fi_d[:k].cpu().numpy().view(np.uint32), fi)
+        assert np.array_equal(rec_d[:k * 74].cpu().numpy().reshape(-1, 74), rec)
+        assert np.array_equal(p.flows(), table)
+
+
 @pytest.mark.parametrize("lib", ["legacy_init_hook", "product"])
 def test_legacy_init_race_pinned(gpu, oracle, lib, monkeypatch):
     """round 5's intermittent all-zero flow ids, made deterministic.
