@@ -10,6 +10,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 case ${LEG:-1M} in
   share) legargs=(--config4 --virtual-world 8) ;;
+  c3) legargs=() ;;  # config 3 (K3 mode 0; K1 counters in the same passes)
   *) legargs=(--config4 --shard contig) ;;
 esac
 args=(--steps 2 --warmup 1 --no-cpu --no-extra --sample-check "${legargs[@]}")
