@@ -698,7 +698,9 @@ int tcbee_parse_batch_device_ex(tcbee_ctx* c, const tcbee_frames* in, const tcbe
     // trade-off: more blocks = more latency hidden; each block writes a partial row
     // of every flow, so a block should see a few thousand records; and a block
     // never covers more than kK3MaxPer records (bin fields cannot overflow)
-    uint64_t g1 = (in->n + 8191) / 8192;
+    // (16384 records per block below n_cu blocks: config 2's step -2.4 % against 8192,
+    //  32768 +11 %, profiles/r06_config2_attempts.log; 4096 / 2048 were slower, round 2)
+    uint64_t g1 = (in->n + 16383) / 16384;
     if (g1 > (uint64_t)c->n_cu) g1 = c->n_cu;
     const uint64_t gmin = (in->n + kK3MaxPer - 1) / kK3MaxPer;
     if (g1 < gmin) g1 = gmin;
