@@ -523,6 +523,15 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
       h[f] = flow_hash64(K[f][0], K[f][1], K[f][2], K[f][3], K[f][4]);
       if (acc[f]) hsh[f] = fold32(h[f]);
       want[f] = uni[f] ? lane == leader[f] : acc[f];
+      // a frame group whose wave-uniform key is frame group 0's too (a hot flow):
+      // no probe of its own, group 0's result below (round 6: config 2's step -2.8 %,
+      // half the probes and inserts of a hot new flow; profiles/r06_config2_attempts.log)
+      if (f > 0 && uni[f] && uni[0]) {
+        bool eq = true;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) eq = eq && K[f][j] == K[0][j];
+        if (__all(!acc[f] || !acc[0] || eq) && __any(acc[f] && acc[0])) want[f] = false;
+      }
       v4k[f] = key_is_v4form(K[f]);
       if (want[f]) {
         // Plain (cacheable) loads are exact here: a claimer stores everything a
@@ -635,7 +644,11 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
                            kFs32Flag | (uint32_t)(i0 + (uint64_t)f * kBlock + tid));
       }
       // a wave-uniform key: the leader's result for the whole wave
-      if (uni[f]) {
+      if (f > 0 && uni[f] && !__any(want[f])) {  // group 0's flow (above)
+        slot[f] = slot[0];
+        claim[f] = claim[0];
+        fs_seen[f] = fs_seen[0];
+      } else if (uni[f]) {
         slot[f] = __shfl(sl, leader[f]);
         claim[f] = __shfl(cl, leader[f]);
         fs_seen[f] = __shfl(fs, leader[f]);
