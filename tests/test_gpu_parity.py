@@ -303,6 +303,29 @@ def test_k3_big_caplen_and_hot_flow(gpu, oracle, flows, nopack, monkeypatch):
         assert p.status() == 0
 
 
+@pytest.mark.parametrize("nopack", ["0", "1"])
+def test_k3_mode1_long_caplens(gpu, oracle, nopack, monkeypatch):
+    """K3 mode 1 (k_count_chunk2) with caplens around every field boundary: < 2047 (the
+    region entry), 2047..16383 (round 6: the chunk sends their bytes to the flow's
+    counter by a device atomic), 16383+ (past the packed K1 -> K3 field), 65536+ and
+    2^20+; asserted to run in mode 1; records, ids and the table (pkts, bytes) exact."""
+    monkeypatch.setenv("TCBEE_TEST_NOPACK", nopack)
+    tr = tcbee_amd.synth_trace(400_000, sizes="imix", kind=1, n_flows=60_000, seed=2047)
+    rng = np.random.default_rng(11)
+    pad = 1_200_000
+    arena = np.concatenate([tr.arena, np.zeros(pad, np.uint8)])
+    ln = tr.caplen.copy()
+    for lo, hi, k in ((2040, 2060, 400), (2047, 16_400, 800), (16_380, 70_000, 300),
+                      ((1 << 20) - 8, (1 << 20) + 100_000, 40)):
+        idx = rng.choice(tr.n, size=k, replace=False)
+        ln[idx] = rng.integers(lo, hi, size=k).astype(np.uint32)
+    tr2 = Trace(arena, tr.offset, ln, tr.ts_ns)
+    with tcbee_amd.PacketParser(max_frames=1 << 19, max_arena=len(arena) + 64,
+                                max_flows=62_000, variants=nopack == "1") as p:
+        assert_same(p.parse(tr2), oracle.parse(tr2), p.flows())
+        assert p.count_mode() == 1 and p.status() == 0
+
+
 @pytest.mark.parametrize("cuts", [[0, 30_000], [0, 9_000, 9_001, 21_000, 30_000],
                                   [0, 3_000, 6_000, 9_000, 12_000, 15_000, 18_000, 21_000, 30_000]])
 def test_device_merge_matches_unsharded(gpu, oracle, cuts):
