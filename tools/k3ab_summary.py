@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-kernel median durations (us) of the K3 kernels in gpurun_out/k3ab_<lib>_<i>/
-kernel traces (tools/r05_k3ab.sh), split by workload in launch order."""
+kernel traces (tools/k3_ab.sh), split by workload in launch order."""
 import csv
 import glob
 import statistics
