@@ -19,7 +19,7 @@ struct tcbee_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   uint64_t max_frames = 0, max_arena = 0, max_flows = 0;
-  int fpl = 2;
+  int fpl = TCBEE_K1_FPL;
   bool reset_pending = false;   // tcbee_flow_reset_device: applied by the next launch
   uint32_t withhold_every = 0;  // TCBEE_TEST_WITHHOLD (look-back recount test hook)
   int k3_no_bucket = 0;         // TCBEE_TEST_K3_NOBUCKET=1: large tables use K3 mode 2 (test hook)
@@ -176,7 +176,7 @@ void dfree(void* p) {
   if (p) (void)hipFree(p);
 }
 
-uint64_t tile_frames(int fpl) { return (uint64_t)kBlock * (uint64_t)fpl; }
+uint64_t tile_frames(int fpl) { return (uint64_t)kK1Block * (uint64_t)fpl; }
 
 int ensure_host_path(tcbee_ctx* c) {
   if (c->d_arena) return TCBEE_OK;

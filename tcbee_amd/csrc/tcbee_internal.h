@@ -341,6 +341,15 @@ hipError_t launch_shard_index(const ShardArgs& a, hipStream_t s);
 hipError_t launch_rss_load(const ShardArgs& a, hipStream_t s);
 
 constexpr int kBlock = 256;
+// K1's block size and the product's frames per lane (build-time A/B knobs; a tile is
+// kK1Block x FPL frames)
+#ifndef TCBEE_K1_BS
+#define TCBEE_K1_BS 256
+#endif
+#ifndef TCBEE_K1_FPL
+#define TCBEE_K1_FPL 2
+#endif
+constexpr int kK1Block = TCBEE_K1_BS;
 static_assert(kShardChunk == (uint64_t)kBlock * kShardPer, "shard chunk = one block");
 constexpr int kScanWordsPerBlock = 2048;  // 256 threads x 8 words
 constexpr uint64_t kRankSmallWords = 1024 * 32;  // single-block rank up to 1M frames

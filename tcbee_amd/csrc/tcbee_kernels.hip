@@ -411,9 +411,9 @@ __device__ __forceinline__ void copy_out(uint8_t* __restrict__ out, uint64_t G0,
 // are staged in LDS at their compacted positions and stored by the whole block
 // after the look-back (a per-wave staging was slightly slower, round 2).
 template <int FPL, bool FLOWS>
-__global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
-  constexpr int TILE = kBlock * FPL;
-  constexpr int NW = kBlock / 64;  // waves per tile
+__global__ __launch_bounds__(kK1Block) void k_parse(ParseArgs a) {
+  constexpr int TILE = kK1Block * FPL;
+  constexpr int NW = kK1Block / 64;  // waves per tile
   constexpr int SREC_DW = (TILE * kRecBytes + 32) / 4;
   __shared__ __attribute__((aligned(16))) uint32_t s_rec[SREC_DW];
   __shared__ uint32_t s_wcnt[FPL][NW];
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   uint64_t offv[FPL], tsv[FPL];
 #pragma unroll
   for (int f = 0; f < FPL; ++f) {
-    const uint64_t i = i0 + (uint64_t)f * kBlock + tid;
+    const uint64_t i = i0 + (uint64_t)f * kK1Block + tid;
     acc[f] = false;
     slot[f] = 0xFFFFFFFFu;
     claim[f] = 0xFFFFFFFFu;
@@ -641,7 +641,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
         }
         if (slow)
           sl = flow_upsert(a.tab, K[f], h[f], a.batch, a.new_list, a.persist, fbase, fs, cl,
-                           kFs32Flag | (uint32_t)(i0 + (uint64_t)f * kBlock + tid));
+                           kFs32Flag | (uint32_t)(i0 + (uint64_t)f * kK1Block + tid));
       }
       // a wave-uniform key: the leader's result for the whole wave
       if (f > 0 && uni[f] && !__any(want[f])) {  // group 0's flow (above)
@@ -680,7 +680,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
   {
     const uint64_t wr_lo = excl < a.out_cap ? excl : a.out_cap;
     const uint64_t wr_hi = (excl + total) < a.out_cap ? (excl + total) : a.out_cap;
-    if (wr_hi > wr_lo) copy_out(a.out_rec, wr_lo * kRecBytes, wr_hi * kRecBytes, s_rec, tid, kBlock);
+    if (wr_hi > wr_lo) copy_out(a.out_rec, wr_lo * kRecBytes, wr_hi * kRecBytes, s_rec, tid, kK1Block);
   }
 
   // ---- per-record side outputs; first_seen = min accepted index ----
@@ -694,7 +694,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
       // (side words non-temporal too: -0.35 % on config 3's K1, round 6)
       if (a.out_hash && p < a.out_cap) __builtin_nontemporal_store(hsh[f], &a.out_hash[p]);
       // record -> frame map (flow-hash shards of traces with rejected frames)
-      if (a.out_frame && p < a.out_cap) a.out_frame[p] = (uint32_t)(i0 + (uint64_t)f * kBlock + tid);
+      if (a.out_frame && p < a.out_cap) a.out_frame[p] = (uint32_t)(i0 + (uint64_t)f * kK1Block + tid);
       if (FLOWS) {
         if (a.pack_bits) {
           // (claim, caplen) in one word; a caplen that does not fit saturates the
@@ -719,7 +719,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(ParseArgs a) {
         const uint32_t leader = (uint32_t)__ffsll((unsigned long long)am) - 1;
         const uint32_t s0 = __shfl(slot[f], leader);
         const uint32_t p32 = (uint32_t)p;
-        const uint32_t frame_i = (uint32_t)(i0 + (uint64_t)f * kBlock + tid);
+        const uint32_t frame_i = (uint32_t)(i0 + (uint64_t)f * kK1Block + tid);
         if (__all(!mine || slot[f] == s0)) {
           // leader = lowest rank of the wave = its smallest accepted index; when the
           // wave's previous frame group was all this slot too, its earlier leader
@@ -2076,18 +2076,25 @@ hipError_t launch_table_init(FlowTable t, hipStream_t s) {
 template <int FPL>
 static hipError_t launch_parse_fpl(const ParseArgs& a, bool flows, hipStream_t s) {
   const dim3 grid((unsigned)a.ntiles);
-  if (flows) hipLaunchKernelGGL((k_parse<FPL, true>), grid, dim3(kBlock), 0, s, a);
-  else hipLaunchKernelGGL((k_parse<FPL, false>), grid, dim3(kBlock), 0, s, a);
+  if (flows) hipLaunchKernelGGL((k_parse<FPL, true>), grid, dim3(kK1Block), 0, s, a);
+  else hipLaunchKernelGGL((k_parse<FPL, false>), grid, dim3(kK1Block), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_parse(const ParseArgs& a, int fpl, bool flows, hipStream_t s) {
   // (FPL 2 in every product context; 1 and 4: test tilings of the variants build)
   switch (fpl) {
-    case 2: return launch_parse_fpl<2>(a, flows, s);
+    case TCBEE_K1_FPL: return launch_parse_fpl<TCBEE_K1_FPL>(a, flows, s);
 #if TCBEE_VARIANTS
+#if TCBEE_K1_FPL != 1
     case 1: return launch_parse_fpl<1>(a, flows, s);
+#endif
+#if TCBEE_K1_FPL != 2
+    case 2: return launch_parse_fpl<2>(a, flows, s);
+#endif
+#if TCBEE_K1_FPL != 4
     case 4: return launch_parse_fpl<4>(a, flows, s);
+#endif
 #endif
     default: return hipErrorInvalidValue;
   }
