@@ -316,6 +316,7 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    t_issue = time.perf_counter()  # the host's issue time (a step rate near it: host-bound)
     torch.cuda.synchronize()
     if multi:
         dist.barrier()
@@ -339,7 +340,8 @@ def run_device(torch, dist, rank, world, n, sizes, kind, n_flows, steps, warmup,
     else:
         flows = (merged if merged is not None else p).flows()
     check = {"records": nrec, "flows": int(len(flows)), "status": status,
-             "pkts_total": int(flows["pkts"].sum())}
+             "pkts_total": int(flows["pkts"].sum()),
+             "host_issue_ms_per_step": round((t_issue - t0) / steps * 1e3, 4)}
     if multi:
         check["ingress_global"] = int(last["ctr"][0].item())
         if fx is not None:

@@ -1165,7 +1165,10 @@ int tcbee_ctx_profile(tcbee_ctx* c, int enable) {
   TRY_HIP(hipSetDevice(c->device));
   if (enable && c->ev.empty()) {
     c->ev.resize(2 * kMaxProfiled, nullptr);
-    for (auto& e : c->ev) TRY_HIP(hipEventCreate(&e));
+    // timing-only events: no system-scope fence (its L2 writeback + invalidate is
+    // measurement overhead between the kernels it brackets; elapsed times are read
+    // after a stream synchronize)
+    for (auto& e : c->ev) TRY_HIP(hipEventCreateWithFlags(&e, TCBEE_PROF_EVFLAGS));
   }
   c->profiling = enable != 0;
   c->ev_used = 0;

@@ -384,6 +384,10 @@ constexpr uint32_t kSmallNb = 512, kStagedMinNb = 64;
 #define TCBEE_K3_CHUNK 12288
 #endif
 constexpr uint32_t kChunk = TCBEE_K3_CHUNK;
+// flags of tcbee_ctx_profile's K1 timing events (A/B knob; 0 = hipEventDefault)
+#ifndef TCBEE_PROF_EVFLAGS
+#define TCBEE_PROF_EVFLAGS hipEventDisableSystemFence
+#endif
 #ifndef TCBEE_K3_CHUNK_BLOCK
 #define TCBEE_K3_CHUNK_BLOCK 512
 #endif

@@ -30,7 +30,8 @@ def main():
                                                  0x7CBEE, full_check=(r == 0))
             key = f"warmup={w} steps={s}"
             res.setdefault(key, []).append((round(el / s * 1e3, 4), round(k1, 4)))
-            print(key, res[key][-1], chk.get("full_bit_exact"), flush=True)
+            print(key, res[key][-1], chk.get("full_bit_exact"), "host issue ms/step",
+                  chk.get("host_issue_ms_per_step"), flush=True)
     print(json.dumps(res))
 
 
