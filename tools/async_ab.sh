@@ -1,3 +1,6 @@
+#!/bin/bash
+# K3 on a side stream beside the next step's K1 (TCBEE_BENCH_ASYNC=1) vs in line, config 3,
+# alternating processes (round 6, profiles/r06_async_ids_ab.log).
 set -u
 mkdir -p gpurun_out
 for i in 1 2; do

@@ -1,3 +1,9 @@
+#!/bin/bash
+# K1 timing-event flags A/B (round 6, profiles/r06_prof_event_ab.log): config 2 per step
+# (tools/c2_ab.sh) and config 3 for three builds, then a kernel trace of the kept one.
+# Build first, here: HIPEXTRA=-DTCBEE_PROF_EVFLAGS=0 tools/lib_ab.sh build wt:evdef;
+# HIPEXTRA=-DTCBEE_PROF_EVFLAGS=hipEventReleaseToDevice tools/lib_ab.sh build wt:evdev;
+# tools/lib_ab.sh build wt:evnf (the default, hipEventDisableSystemFence).
 set -u
 mkdir -p gpurun_out
 NAMES="wt_evdef wt_evnf wt_evdev" PAIRS=3 timeout -k 10 300 bash tools/c2_ab.sh > gpurun_out/ev_c2.log 2>&1 || exit 1
