@@ -5,7 +5,7 @@ every other seed; each trace through one batch and through three batches of a ke
 table, everything bit-exact vs the oracle. Prints one line per seed and a summary;
 exits 1 on the first mismatch.
 
-  python tools/fuzz_soak.py [--seeds 60] [--frames 300000]
+  python tools/fuzz_soak.py [--seeds 60] [--seed0 1000] [--frames 300000]
 """
 import argparse
 import os
@@ -32,6 +32,7 @@ def same(res, orc, flows=None, table=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seeds", type=int, default=60)
+    ap.add_argument("--seed0", type=int, default=1000, help="first seed")
     ap.add_argument("--frames", type=int, default=300_000)
     a = ap.parse_args()
     import tcbee_amd
@@ -41,7 +42,7 @@ def main():
     pools = [0, 40, 3000, 60_000]
     t0 = time.time()
     frames = 0
-    for seed in range(1000, 1000 + a.seeds):
+    for seed in range(a.seed0, a.seed0 + a.seeds):
         pool = pools[seed % len(pools)]
         port = 4242 if seed % 2 else 0
         n = a.frames
