@@ -127,6 +127,33 @@ def test_config2_1M_bit_exact(parser, oracle):
     assert len(fl) == 1 and int(fl["pkts"][0]) == 1_000_000 and int(fl["first_seen"][0]) == 0
 
 
+def test_k1_profiling_events(parser, oracle):
+    """tcbee_ctx_profile (bench.py's live K1 timing): one event pair per
+    K1 launch, timing-only events (no system-scope fence) whose durations are positive
+    and fit inside the wall time of the synchronized calls; profiling changes no output,
+    and a profile(False) context records nothing."""
+    import time
+    import torch
+    tr = tcbee_amd.synth_trace(500_000, sizes="imix", kind=1, n_flows=2000)
+    orc = oracle.parse(tr)
+    parser.profile(False)
+    assert parser.profile_read() == (0.0, 0)
+    parser.profile(True)
+    walls = []
+    for _ in range(3):
+        parser.reset_flows()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = parser.parse(tr)
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t0)
+        assert_same(res, orc, parser.flows())
+    ms, k = parser.profile_read()
+    parser.profile(False)
+    assert k == 3
+    assert 0.0 < ms <= sum(walls) * 1e3
+
+
 def test_config3_imix_multiflow(parser, oracle):
     tr = tcbee_amd.synth_trace(300_000, sizes="imix", kind=1, n_flows=10_000)
     parser.reset_flows()
