@@ -1,18 +1,12 @@
 """Multi-rank path on CPU: world-size-2 gloo run of the shard + table-exchange
 choreography (tcbee_amd.dist) against the oracle on the unsharded trace."""
 import os
-import socket
 
 import numpy as np
 import pytest
 
 
-def free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+from ports import free_port  # noqa: E402
 
 
 def test_shard_range_covers_everything():

@@ -12,7 +12,6 @@ the one the driver records.
 """
 import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -22,12 +21,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+from ports import free_port  # noqa: E402
 
 
 def launch(world: int, args: list[str], timeout: int, **env_extra):

@@ -4,7 +4,6 @@ remap choreography, on one stream (FlowMerge.step) and overlapped with the
 next step's parse on a side stream (OverlappedMerge, as bench.py). Records,
 global flow ids, global counters and the merged table vs the oracle on the
 unsharded trace."""
-import socket
 
 import numpy as np
 import pytest
@@ -12,12 +11,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+from ports import free_port  # noqa: E402
 
 
 @pytest.mark.parametrize("mode", ["step", "overlap", "owner"])
